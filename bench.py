@@ -1,0 +1,227 @@
+#!/usr/bin/env python
+"""bench.py — Mrays/s + ms/frame of mirror-maze's ray-trace loop on MI355X.
+
+Headline workload (BASELINE.json configs[2], "C3"): 32x32 maze, 1920x1080,
+8 spp, bounce_limit 8, mirror_limit 8.  A "step" is one full frame: every
+pixel x sample path traced through the HIP kernels (no work skipped), frame
+index = step number (fresh RNG every step).  A "ray" is one closest-hit BVH
+query (src/shaders.metal:307).
+
+N GPUs (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+the frame's rows are interleaved over ranks (rank r renders rows r, r+N, ...),
+and rank 0 receives every tile with one RCCL gather per frame (north star:
+"tiles of the framebuffer shard one-per-GPU ... single RCCL gather at frame
+end").  Total work is fixed as N grows -> "scaling": "strong".
+
+Prints ONE JSON line on rank 0 (driver contract), with the roofline of the
+dominant kernel (HIP-event timed inside the timed region) and a CPU baseline
+(the oracle restatement on a bounded row sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "mirror-maze_amd"))
+sys.path.insert(0, str(REPO))
+
+CONFIGS = {
+    # id: (maze_n, W, H, spp, bounce_limit, mirror_limit, description)
+    "c2": (16, 1920, 1080, 1, 4, 15, "C2: 16x16 maze, 1920x1080, 1 spp, 4 bounces"),
+    "c3": (32, 1920, 1080, 8, 8, 8, "C3: 32x32 maze, 1920x1080, 8 spp, 8 mirror bounces"),
+    "c4": (32, 3840, 2160, 16, 8, 15, "C4: 32x32 maze, 3840x2160, 16 spp, 8 bounces"),
+}
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, non-packed fp32 ops
+BYTES_PER_RAY = 136            # SoA path state read+write + hit record
+BYTES_PER_PIXEL = 16           # float4 output
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--pipeline", default="auto", choices=["auto", "mega", "wave"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (approx)")
+    return p.parse_args()
+
+
+def cpu_baseline(scene, u, ext, W, H, budget_s):
+    """Oracle (CPU restatement, oracle/mm_oracle.c -O2 scalar) on a bounded row
+    sample of the same workload, one thread per core, GIL released in C."""
+    from oracle.oracle import Oracle
+
+    o = Oracle.from_scene(scene)
+    threads = max(1, min(16, (os.cpu_count() or 1)))
+    # calibrate on one row, then pick a row sample that fits the budget
+    t0 = time.perf_counter()
+    _, st = o.trace_tile(u, ext, 0, H // 2, W, 1)
+    row_s = max(time.perf_counter() - t0, 1e-6)
+    rows = int(max(threads, min(H, budget_s * threads / row_s)))
+    stride = max(1, H // rows)
+    sample_rows = list(range(0, H, stride))[:rows]
+    totals = [0] * threads
+    lock = threading.Lock()
+    work = list(sample_rows)
+
+    def worker(i):
+        while True:
+            with lock:
+                if not work:
+                    return
+                y = work.pop()
+            _, s = o.trace_tile(u, ext, 0, y, W, 1)
+            totals[i] += s.rays
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    rays = sum(totals)
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{len(sample_rows)} of {H} rows (every {stride}th) x {W} px x {ext.spp} spp, "
+                      f"{rays} rays in {dt:.1f} s; scalar C oracle -O2 -ffp-contract=off"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from mirror_maze import MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, Renderer, Scene
+    from mirror_maze import default_uniform, make_ext
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    maze_n, W, H, spp, bl, ml, desc = CONFIGS[args.config]
+    scene = Scene.build(maze_n, 0)
+    ren = Renderer(local)
+    ren.set_pipeline({"auto": MM_PIPE_AUTO, "mega": MM_PIPE_MEGAKERNEL, "wave": MM_PIPE_WAVEFRONT}[args.pipeline])
+    ren.upload_scene(scene)
+    stream = torch.cuda.current_stream(dev)
+    ren.set_stream(stream)
+    u = default_uniform(W, H, 0)
+
+    # rows r, r+world, ... ; pad so every rank sends the same shape
+    rows_max = (H + world - 1) // world
+    my_rows = len(range(rank, H, world))
+    tile = torch.zeros((rows_max, W, 4), dtype=torch.float32, device=dev)
+    gathered = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+
+    def step(frame, stats=False):
+        ext = make_ext(spp, bl, ml, frame=frame)
+        _, st = ren.trace_tile(u, ext, 0, rank, W, my_rows, y_stride=world, out=tile[:my_rows], stats=stats)
+        if world > 1:
+            dist.gather(tile, gathered, dst=0)
+            if rank == 0:  # de-interleave: row i*world + r <- gathered[r][i]
+                full = torch.stack(gathered, dim=1).reshape(rows_max * world, W, 4)
+                frame_buf.copy_(full[:H])
+        elif rank == 0:
+            frame_buf.copy_(tile[:H])
+        return st
+
+    for i in range(args.warmup):
+        step(10_000 + i)
+    ren.set_profiling(True)
+    ren.kernel_timing(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    k_ms, k_launches = ren.kernel_timing(reset=True)
+    ren.set_profiling(False)
+
+    # count the rays of exactly the timed frames (deterministic re-run, untimed)
+    rays = paths = visits = rtests = 0
+    for i in range(args.steps):
+        st = step(i, stats=True)
+        rays += st.rays; paths += st.paths; visits += st.node_visits; rtests += st.rect_tests
+    counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
+    t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+    rays_all, paths_all, visits_all, rtests_all = (float(x) for x in counts.tolist())
+    elapsed = float(t_el.item())
+
+    if rank == 0:
+        img = frame_buf.cpu().numpy()
+        assert np.isfinite(img).all(), "non-finite pixels"
+        value = rays_all / elapsed / 1e6
+        # roofline of the dominant kernel (ray trace), rank 0's launches
+        k_avg_s = (k_ms / 1e3) / max(k_launches, 1)
+        rays_per_launch = rays / max(k_launches, 1)            # rank-0 rays over its launches
+        pix_per_launch = (my_rows * W * args.steps) / max(k_launches, 1)
+        alg_bytes = BYTES_PER_RAY * rays_per_launch + BYTES_PER_PIXEL * pix_per_launch
+        achieved = alg_bytes / k_avg_s / 1e9
+        traffic = None
+        tf = REPO / "profiles" / f"traffic_{args.config}_{args.pipeline}.json"
+        if tf.exists():
+            traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+        valu_ops = (25 * 2 * (visits / max(k_launches, 1)) + 71 * (rtests / max(k_launches, 1)))
+        line = {
+            "metric": "Mrays/sec + ms/frame at 1920x1080, 8 spp, 8 bounces; 1/2/4/8-GPU scaling",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: Kruskal maze seed 0 (host C++ restatement), default camera, RNG keyed (pixel,sample,frame)",
+            "config": {"workload": desc, "maze_n": maze_n, "width": W, "height": H, "spp": spp,
+                       "bounce_limit": bl, "mirror_limit": ml, "pipeline": args.pipeline,
+                       "parallelism": f"rows interleaved x{world} + RCCL gather" if world > 1 else "1 GPU",
+                       "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),
+                       "node_visits_per_ray": round(visits_all / max(rays_all, 1), 2),
+                       "rect_tests_per_ray": round(rtests_all / max(rays_all, 1), 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "trace", "kernel_avg_ms": round(k_avg_s * 1e3, 3), "launches": k_launches,
+                         "bytes_per_ray": BYTES_PER_RAY,
+                         "valu": {"achieved_tops": round(valu_ops / k_avg_s / 1e12, 3), "peak_tops": VALU_PEAK_TOPS,
+                                  "frac": round(valu_ops / k_avg_s / 1e12 / VALU_PEAK_TOPS, 4),
+                                  "ops": "25 per AABB test + 71 per rect test (SURVEY 8d)"}},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(scene, u, make_ext(spp, bl, ml, frame=0), W, H, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    ren.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+/*
+ * mm_api.h — the drop-in boundary: a C ABI over the MI355X (gfx950) HIP
+ * implementation of mirror-maze's per-pixel ray-trace loop.
+ *
+ * Reference interface replaced (all paths relative to the reference repo):
+ *   - the Metal compute dispatch of `compute_shader`
+ *       kernel signature        src/shaders.metal:245-259
+ *       argument table binding  src/main.rs:870-883  (set_buffer 0..6,
+ *                               set_bytes(4, Uniform), set_texture 0/1)
+ *       dispatch                src/main.rs:884-885  (32x24 groups of 32x32)
+ *   - the Metal buffer plumbing  src/utils.rs:86-102 (make_buf/copy_to_buf)
+ *   - device/queue creation      src/main.rs:616-626, 638-640
+ *
+ * Conventions: 0 on success, a negative MM_ERR_* code otherwise (message via
+ * mm_last_error); no exceptions or aborts cross the ABI; host memory is owned
+ * by the caller and copied; device memory is owned by the context unless a
+ * function says it writes into a caller-provided device pointer.  A context is
+ * bound to one GPU and is not thread-safe (the reference drives Metal from one
+ * main thread too, src/main.rs:591).  All work is enqueued on the context's
+ * stream; mm_sync waits for it (the reference never waits, src/main.rs:894).
+ */
+#ifndef MM_API_H
+#define MM_API_H
+
+#include "mm_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mm_ctx mm_ctx;
+
+/* Library version, e.g. "mirror-maze-amd 0.1 gfx950". */
+const char* mm_version(void);
+
+/* Replaces Device::system_default() + new_command_queue (main.rs:616-623).
+ * device: HIP ordinal.  The context owns a non-blocking stream. */
+int  mm_create(int device, mm_ctx** out);
+void mm_destroy(mm_ctx* ctx);
+const char* mm_last_error(const mm_ctx* ctx);
+
+/* Enqueue on a caller stream (hipStream_t passed as void*), e.g. torch's
+ * current stream; NULL restores the context's own stream. */
+int  mm_set_stream(mm_ctx* ctx, void* hip_stream);
+
+/* Replaces make_buf for buffers 1,2,3,5,6 (main.rs:725-730):
+ *   rects      buffer 1  mirrors      n_rects x 48 B
+ *   nodes      buffer 2  nodes        n_nodes x 32 B
+ *   idx        buffer 3  indices      n_rects x u32
+ *   is_mirror  buffer 5  materials    n_rects x 1 B (bool)
+ *   emission   buffer 6  emissions    n_rects x float4
+ * Copies the data; validates the tree (indices in range, stack depth <= 50). */
+int  mm_upload_scene(mm_ctx* ctx,
+                     const mm_rect* rects, uint32_t n_rects,
+                     const mm_node* nodes, uint32_t n_nodes,
+                     const uint32_t* idx,
+                     const uint8_t* is_mirror,
+                     const float* emission);
+
+/* ---- parity mode: the reference dispatch, bit for bit --------------------
+ * Replaces copy_to_buf(chunks) + dispatch_thread_groups (main.rs:778-885).
+ * Launches (view_w/2/ppc) x (view_h/2/ppc) reference threadgroups of 32x32
+ * threads (ppc = chunk_w^2 = 16, 64 samples per pixel); threadgroup g reads
+ * chunk origin chunks[g] (uint2, buffer 0) and writes 16 texels of the
+ * context's framebuffer (the `texout` texture, RGBA; never cleared, like the
+ * reference's Private screen texture).  n_chunks must cover the grid. */
+int  mm_trace_chunks(mm_ctx* ctx, const mm_uniform* uni,
+                     const uint32_t* chunks, uint32_t n_chunks);
+
+/* Download the framebuffer (view_w x view_h, row-major, y down).
+ * rgba_f32: 4 floats/texel before unorm quantisation (alpha = 1), or NULL;
+ * rgba8:    RGBA8Unorm as the texture stores it (round-to-nearest-even of
+ *           clamp(x,0,1)*255), or NULL. */
+int  mm_read_framebuffer(mm_ctx* ctx, float* rgba_f32, uint8_t* rgba8);
+
+/* ---- throughput mode: offline renderer ------------------------------------
+ * Renders pixels (x0 + i, y0 + j*y_stride), 0<=i<w, 0<=j<h, of the frame
+ * uni->view_w x uni->view_h with ext->spp samples each, ext->bounce_limit /
+ * ext->mirror_limit, RNG keyed on (pixel, sample, ext->frame) so any tiling
+ * over any number of GPUs reproduces the 1-GPU image bit for bit.
+ * out_dev: caller DEVICE pointer to w*h float4 (row-major over (j,i));
+ * alpha = 1 (or, with MM_EXT_ACCUMULATE, += the frame value, alpha += 1).
+ * stats: optional host pointer; filled after an implicit sync when
+ * MM_EXT_COUNT_STATS is set. */
+int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
+                   uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                   uint32_t y_stride, float* out_dev, mm_stats* stats);
+
+/* Pipeline selection for mm_trace_tile (MM_PIPE_AUTO picks the fastest). */
+#define MM_PIPE_AUTO       0
+#define MM_PIPE_MEGAKERNEL 1   /* one thread per path, bounce loop in-kernel */
+#define MM_PIPE_WAVEFRONT  2   /* SoA path state + compacted ray queues      */
+int  mm_set_pipeline(mm_ctx* ctx, int pipe);
+
+/* Wait for all work queued by this context. */
+int  mm_sync(mm_ctx* ctx);
+
+/* Per-kernel timing of the dominant (ray-trace) kernel: when enabled, every
+ * trace-kernel launch is bracketed by HIP events on the context's stream.
+ * mm_kernel_timing syncs, returns the summed ms and the launch count since the
+ * last reset, and optionally resets. */
+int  mm_set_profiling(mm_ctx* ctx, int enable);
+int  mm_kernel_timing(mm_ctx* ctx, float* total_ms, uint32_t* launches, int reset);
+
+/* Device-side timing of the last mm_trace_tile / mm_trace_chunks call,
+ * measured with HIP events on the context's stream (ms), and the number of
+ * kernel launches it made. */
+int  mm_last_timing(mm_ctx* ctx, float* ms, uint32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MM_API_H */

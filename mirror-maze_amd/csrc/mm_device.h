@@ -1,0 +1,138 @@
+// mm_device.h — device-side data layout and IEEE-exact helpers shared by the
+// mirror-maze HIP kernels.  Compiled only by hipcc for gfx950, with
+// -ffp-contract=off: every + - * rounds separately and / and sqrtf are the
+// correctly rounded expansions (hipcc's default
+// -fhip-fp32-correctly-rounded-divide-sqrt), so the device arithmetic is the
+// reference kernel's AIR arithmetic with IEEE intrinsics.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mm_types.h"
+
+namespace mm {
+
+constexpr float kBig = 1e30f;     // shaders.metal:15, 94, 149 (IR 0x46293E5940000000)
+constexpr int kStackMax = 50;     // shaders.metal:123
+
+// ---- HBM layouts ------------------------------------------------------------
+// Node: 2 x float4 = the reference's 32-B bvh_node, re-typed for 16-B loads:
+//   a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(left_first), bits(count))
+// Children of an interior node are adjacent (left_first, left_first+1), so the
+// pair a traversal step reads is one contiguous 64-B line.
+//
+// Rect geometry: 4 x float4 per rect (64 B):
+//   g0 = (o.xyz, |v|)  g1 = (n.xyz, |u|)  g2 = (v.xyz, kind)  g3 = (u.xyz, 0)
+// n, |v|, |u| are the per-rect subexpressions of ray_rect_intersect
+// (shaders.metal:52,60,61), computed once by k_prep_rects with the same ops.
+// Shade record: s0 = (color.rgb, is_mirror), s1 = emission (rgba).
+struct DevScene {
+    const float4* nodes;      // 2 * n_nodes
+    const float4* geo;        // 4 * n_rects
+    const float4* shade;      // 2 * n_rects
+    const uint32_t* idx;      // n_rects
+    uint32_t n_nodes;
+    uint32_t n_rects;
+};
+
+// ---- IEEE helpers (the AIR intrinsics with their IEEE meaning) -------------
+struct F3 { float x, y, z; };
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 operator+(F3 a, F3 b) { return F3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ F3 operator-(F3 a, F3 b) { return F3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ F3 operator*(F3 a, F3 b) { return F3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ F3 operator*(float s, F3 a) { return F3{s * a.x, s * a.y, s * a.z}; }
+// air.dot.v3f32 = (x*x' + y*y') + z*z'
+__device__ __forceinline__ float dot3(F3 a, F3 b) {
+    float s = a.x * b.x;
+    s = s + a.y * b.y;
+    return s + a.z * b.z;
+}
+// air.fast_rsqrt.f32 -> correctly rounded sqrt, then correctly rounded 1/x
+__device__ __forceinline__ float rsq(float x) { return 1.0f / sqrtf(x); }
+__device__ __forceinline__ F3 normalize3(F3 v) { return rsq(dot3(v, v)) * v; }
+// cross(v, u) in the IR's operand order (ray_rect_intersect %22-%32)
+__device__ __forceinline__ F3 cross3(F3 v, F3 u) {
+    return F3{u.z * v.y - u.y * v.z, u.x * v.z - u.z * v.x, u.y * v.x - u.x * v.y};
+}
+__device__ __forceinline__ F3 xyz(float4 a) { return F3{a.x, a.y, a.z}; }
+
+// (random(state) - 0.5) * 2, shaders.metal:181-186 as folded by the IR
+// (%163-%174): u32 -> f32 (round to nearest) * 2^-31 - 1.
+__device__ __forceinline__ float rand_pm1(uint32_t& state) {
+    uint32_t s = state * 747796405u + 291336453u;
+    state = s;
+    uint32_t r = ((s >> ((s >> 28) + 4u)) ^ s) * 277803737u;
+    r = (r >> 22) ^ r;
+    return (float)r * 0x1p-31f - 1.0f;
+}
+
+// air.convert.u.i32.f.f32: truncation, saturating, NaN -> 0
+__device__ __forceinline__ uint32_t cvt_u32_sat(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+
+// Seed, shaders.metal:288-298 (IR %143-%161).  The sampler (repeat,
+// nearest, normalized) reads texel (0,0) of noiseTexture-2.png for every
+// integer gid: (128,128,128,255)/255.
+__device__ __forceinline__ uint32_t seed_reference(uint32_t tx, uint32_t ty, uint32_t time) {
+    const float n = 128.0f / 255.0f;
+    float s = n + (float)(tx * 15823u);
+    s = s + n;
+    s = s + (float)(ty * 9737333u);
+    s = s + (float)time;
+    return cvt_u32_sat(s);
+}
+
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
+    uint32_t s = v * 747796405u + 2891336453u;
+    uint32_t w = ((s >> ((s >> 28) + 4u)) ^ s) * 277803737u;
+    return (w >> 22) ^ w;
+}
+// Throughput-mode seed: a function of (pixel, sample, frame) only.
+__device__ __forceinline__ uint32_t seed_tile(uint32_t pixel, uint32_t sample, uint32_t frame) {
+    return pcg_hash(pcg_hash(pcg_hash(frame) ^ pixel) + sample);
+}
+
+// Primary ray direction, shaders.metal:281-284 in IR order (camera centre
+// cancels; quat_mult inlined as %97-%140, %190-%191).
+__device__ __forceinline__ F3 primary_dir(const mm_uniform& u, uint32_t px, uint32_t py) {
+    const float fx = (float)px, fy = (float)py;
+    const float vx = u.cam.viewport[0], vy = u.cam.viewport[1];
+    F3 p = F3{(vx * fx) / u.view_w - vx * 0.5f, (vy * fy) / u.view_h - vy * 0.5f, 0.0f - (-u.cam.focal)};
+    F3 d = normalize3(p);
+    const F3 q = F3{u.cam.quat[0], u.cam.quat[1], u.cam.quat[2]};
+    const float qw = u.cam.quat[3];
+    const F3 nq = F3{-q.x, -q.y, -q.z};
+    const float s1 = -dot3(nq, d);
+    const F3 c1 = F3{nq.y * d.z - nq.z * d.y, nq.z * d.x - nq.x * d.z, nq.x * d.y - nq.y * d.x};
+    const F3 v1 = c1 + qw * d;
+    const F3 c2 = F3{v1.y * q.z - v1.z * q.y, v1.z * q.x - v1.x * q.z, v1.x * q.y - v1.y * q.x};
+    return (qw * v1 + s1 * q) + c2;
+}
+
+// beam.dir = ray_dir + (rand, rand, 0) * 0.001 (shaders.metal:303, IR %189-%192)
+__device__ __forceinline__ F3 jitter(F3 d, uint32_t& seed) {
+    const float j1 = rand_pm1(seed);
+    const float j2 = rand_pm1(seed);
+    return d + F3{j1 * 0.001f, j2 * 0.001f, 0.0f * 0.001f};
+}
+
+// Metal sign(): 1, -1, +-0 for +-0, 0 for NaN
+__device__ __forceinline__ float msign(float x) {
+    if (x > 0.0f) return 1.0f;
+    if (x < 0.0f) return -1.0f;
+    if (x != x) return 0.0f;
+    return x;
+}
+
+// RGBA8Unorm store conversion: round-to-nearest-even of clamp(x,0,1)*255.
+__device__ __forceinline__ uint32_t unorm8(float x) {
+    x = fminf(fmaxf(x, 0.0f), 1.0f);
+    return (uint32_t)rintf(x * 255.0f);
+}
+
+}  // namespace mm

@@ -1,0 +1,33 @@
+// mm_launch.h — host-callable launchers for the kernels in trace_*.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "mm_device.h"
+
+namespace mm {
+
+// Per-rect derived data for the scene (n, |v|, |u|, kind) from raw rects.
+hipError_t launch_prep_rects(const mm_rect* rects_dev, uint32_t n, float4* geo_dev, hipStream_t s);
+
+// Parity mode: the reference dispatch (grid_w x grid_h groups of 32x32).
+hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const uint32_t* chunks_dev,
+                               uint32_t grid_w, uint32_t grid_h, float4* fb, uint32_t* fb8,
+                               unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
+
+struct TileJob {
+    mm_uniform u;
+    mm_ext e;
+    uint32_t x0, y0, w, h, y_stride;
+    uint32_t view_w;     // (uint32_t)u.view_w — pixel index stride
+};
+
+// Throughput mode, megakernel: one thread per (pixel, sample) path; writes
+// the per-sample value sqrt(max(L,0)) to samples[path] (path = pixel*spp+s).
+hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples,
+                             unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
+
+// Per-pixel reduction of spp samples in the reference's order, then / spp.
+hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);
+
+}  // namespace mm

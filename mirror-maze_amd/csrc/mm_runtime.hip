@@ -1,0 +1,392 @@
+// mm_runtime.hip — the C ABI of include/mm_api.h over the HIP runtime.
+//
+// Replaces the reference's Metal plumbing: device/queue creation
+// (src/main.rs:616-626), buffer creation and updates (src/utils.rs:86-102,
+// src/main.rs:723-730, 784) and the compute dispatch (src/main.rs:867-886).
+// No exception or abort crosses the ABI; every HIP error becomes
+// MM_ERR_HIP with the runtime's message in mm_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mm_api.h"
+#include "mm_launch.h"
+
+using namespace mm;
+
+struct mm_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // scene (buffers 1,2,3,5,6 of compute_shader)
+    mm_rect* d_rects = nullptr;
+    float4* d_nodes = nullptr;
+    float4* d_geo = nullptr;
+    float4* d_shade = nullptr;
+    uint32_t* d_idx = nullptr;
+    uint32_t n_rects = 0, n_nodes = 0;
+    bool has_scene = false;
+    // texout (parity mode)
+    float4* d_fb = nullptr;
+    uint32_t* d_fb8 = nullptr;
+    uint32_t fb_w = 0, fb_h = 0;
+    // chunk list (buffer 0)
+    uint32_t* d_chunks = nullptr;
+    size_t chunks_cap = 0;
+    // per-sample staging (throughput mode)
+    float4* d_samples = nullptr;
+    size_t samples_cap = 0;
+    // aux: stats[4] (u64) + error flag (u32)
+    unsigned long long* d_aux = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.0f;
+    uint32_t last_launches = 0;
+    int pipe = MM_PIPE_AUTO;
+    // per-kernel profiling of the trace kernel (mm_set_profiling)
+    bool prof = false;
+    std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
+    size_t prof_used = 0;              // events recorded since last reset
+};
+
+namespace {
+
+int fail(mm_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPC(ctx, expr)                                                                           \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return fail((ctx), MM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+template <typename T>
+int ensure(mm_ctx* c, T*& ptr, size_t& cap, size_t n) {
+    if (n <= cap && ptr) return MM_OK;
+    if (ptr) { (void)hipFree(ptr); ptr = nullptr; cap = 0; }
+    HIPC(c, hipMalloc((void**)&ptr, std::max<size_t>(n, 1) * sizeof(T)));
+    cap = n;
+    return MM_OK;
+}
+
+DevScene dev_scene(const mm_ctx* c) {
+    DevScene s;
+    s.nodes = c->d_nodes;
+    s.geo = c->d_geo;
+    s.shade = c->d_shade;
+    s.idx = c->d_idx;
+    s.n_nodes = c->n_nodes;
+    s.n_rects = c->n_rects;
+    return s;
+}
+
+void free_scene(mm_ctx* c) {
+    (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_geo);
+    (void)hipFree(c->d_shade); (void)hipFree(c->d_idx);
+    c->d_rects = nullptr; c->d_nodes = nullptr; c->d_geo = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
+    c->has_scene = false;
+}
+
+// Stack depth the near-first traversal can reach: at most one pending far
+// child per level, so the tree depth bounds it.
+int check_tree(const mm_node* nodes, uint32_t n_nodes, const uint32_t* idx, uint32_t n_rects, std::string& why) {
+    for (uint32_t i = 0; i < n_rects; ++i)
+        if (idx[i] >= n_rects) { why = "idx out of range"; return MM_ERR_INVALID; }
+    std::vector<std::pair<uint32_t, uint32_t>> todo{{0u, 0u}};
+    std::vector<uint8_t> seen(n_nodes, 0);
+    uint32_t maxd = 0;
+    while (!todo.empty()) {
+        auto [n, d] = todo.back();
+        todo.pop_back();
+        if (n >= n_nodes || seen[n]) { why = "node graph is not a tree"; return MM_ERR_INVALID; }
+        seen[n] = 1;
+        maxd = std::max(maxd, d);
+        const mm_node& nd = nodes[n];
+        if (nd.count > 0) {
+            if ((uint64_t)nd.left_first + nd.count > n_rects) { why = "leaf range out of bounds"; return MM_ERR_INVALID; }
+        } else {
+            if ((uint64_t)nd.left_first + 1 >= n_nodes) { why = "child index out of range"; return MM_ERR_INVALID; }
+            todo.push_back({nd.left_first, d + 1});
+            todo.push_back({nd.left_first + 1, d + 1});
+        }
+    }
+    if (maxd > (uint32_t)kStackMax) { why = "BVH deeper than the 50-entry traversal stack"; return MM_ERR_STACK; }
+    return MM_OK;
+}
+
+int begin_timing(mm_ctx* c) {
+    HIPC(c, hipEventRecord(c->ev0, c->stream));
+    return MM_OK;
+}
+int end_timing(mm_ctx* c, uint32_t launches) {
+    HIPC(c, hipEventRecord(c->ev1, c->stream));
+    c->last_launches = launches;
+    c->last_ms = -1.0f;  // resolved lazily in mm_last_timing
+    return MM_OK;
+}
+
+// Bracket one trace-kernel launch with events when profiling is on.
+int prof_mark(mm_ctx* c) {
+    if (!c->prof) return MM_OK;
+    if (c->prof_used == c->prof_ev.size()) {
+        hipEvent_t e;
+        HIPC(c, hipEventCreate(&e));
+        c->prof_ev.push_back(e);
+    }
+    HIPC(c, hipEventRecord(c->prof_ev[c->prof_used++], c->stream));
+    return MM_OK;
+}
+
+int read_aux(mm_ctx* c, mm_stats* st) {
+    unsigned long long h[5];
+    HIPC(c, hipMemcpyAsync(h, c->d_aux, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (st) { st->rays = h[0]; st->node_visits = h[1]; st->rect_tests = h[2]; st->paths = h[3]; }
+    if ((uint32_t)h[4] != 0) return fail(c, MM_ERR_STACK, "traversal stack overflow (depth > 50)");
+    return MM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mm_version(void) { return "mirror-maze-amd 0.1 gfx950"; }
+
+int mm_create(int device, mm_ctx** out) {
+    if (!out) return MM_ERR_INVALID;
+    *out = nullptr;
+    mm_ctx* c = new (std::nothrow) mm_ctx();
+    if (!c) return MM_ERR_NOMEM;
+    c->device = device;
+    int rc = MM_OK;
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == MM_OK) rc = fail(c, MM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    int n = 0;
+    chk(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    if (rc == MM_OK && (device < 0 || device >= n)) rc = fail(c, MM_ERR_INVALID, "no such HIP device");
+    if (rc == MM_OK) chk(hipSetDevice(device), "hipSetDevice");
+    if (rc == MM_OK) chk(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (rc == MM_OK) chk(hipEventCreate(&c->ev0), "hipEventCreate");
+    if (rc == MM_OK) chk(hipEventCreate(&c->ev1), "hipEventCreate");
+    if (rc == MM_OK) chk(hipMalloc((void**)&c->d_aux, 8 * sizeof(unsigned long long)), "hipMalloc(aux)");
+    if (rc == MM_OK) chk(hipMemset(c->d_aux, 0, 8 * sizeof(unsigned long long)), "hipMemset(aux)");
+    if (rc != MM_OK) {
+        fprintf(stderr, "mm_create: %s\n", c->err.c_str());
+        mm_destroy(c);
+        return rc;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return MM_OK;
+}
+
+void mm_destroy(mm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
+    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux);
+    for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char* mm_last_error(const mm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mm_set_stream(mm_ctx* c, void* s) {
+    if (!c) return MM_ERR_INVALID;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return MM_OK;
+}
+
+int mm_set_pipeline(mm_ctx* c, int pipe) {
+    if (!c || pipe < MM_PIPE_AUTO || pipe > MM_PIPE_WAVEFRONT) return MM_ERR_INVALID;
+    c->pipe = pipe;
+    return MM_OK;
+}
+
+int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
+                    const uint32_t* idx, const uint8_t* is_mirror, const float* emission) {
+    if (!c) return MM_ERR_INVALID;
+    if (!rects || !nodes || !idx || !is_mirror || !emission || n_rects == 0 || n_nodes == 0)
+        return fail(c, MM_ERR_INVALID, "mm_upload_scene: null array or empty scene");
+    if (n_nodes > 2 * n_rects) return fail(c, MM_ERR_INVALID, "mm_upload_scene: more than 2n-1 nodes");
+    std::string why;
+    int rc = check_tree(nodes, n_nodes, idx, n_rects, why);
+    if (rc != MM_OK) return fail(c, rc, "mm_upload_scene: " + why);
+    HIPC(c, hipSetDevice(c->device));
+    free_scene(c);
+    std::vector<float4> shade(2 * (size_t)n_rects);
+    for (uint32_t k = 0; k < n_rects; ++k) {
+        shade[2 * k] = make_float4(rects[k].color[0], rects[k].color[1], rects[k].color[2], is_mirror[k] ? 1.0f : 0.0f);
+        shade[2 * k + 1] = make_float4(emission[4 * k], emission[4 * k + 1], emission[4 * k + 2], emission[4 * k + 3]);
+    }
+    HIPC(c, hipMalloc((void**)&c->d_rects, n_rects * sizeof(mm_rect)));
+    HIPC(c, hipMalloc((void**)&c->d_nodes, n_nodes * sizeof(mm_node)));
+    HIPC(c, hipMalloc((void**)&c->d_geo, 4 * (size_t)n_rects * sizeof(float4)));
+    HIPC(c, hipMalloc((void**)&c->d_shade, 2 * (size_t)n_rects * sizeof(float4)));
+    HIPC(c, hipMalloc((void**)&c->d_idx, n_rects * sizeof(uint32_t)));
+    HIPC(c, hipMemcpyAsync(c->d_rects, rects, n_rects * sizeof(mm_rect), hipMemcpyHostToDevice, c->stream));
+    // mm_node is exactly two float4: (mn.xyz, mx.x) (mx.yz, left_first, count)
+    HIPC(c, hipMemcpyAsync(c->d_nodes, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_idx, idx, n_rects * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));  // host arrays may be freed on return
+    c->n_rects = n_rects;
+    c->n_nodes = n_nodes;
+    c->has_scene = true;
+    return MM_OK;
+}
+
+int mm_trace_chunks(mm_ctx* c, const mm_uniform* u, const uint32_t* chunks, uint32_t n_chunks) {
+    if (!c) return MM_ERR_INVALID;
+    if (!c->has_scene) return fail(c, MM_ERR_NO_SCENE, "mm_trace_chunks: no scene uploaded");
+    if (!u || !chunks) return fail(c, MM_ERR_INVALID, "mm_trace_chunks: null argument");
+    if (!(u->view_w >= 1.0f && u->view_w <= 65536.0f && u->view_h >= 1.0f && u->view_h <= 65536.0f))
+        return fail(c, MM_ERR_INVALID, "mm_trace_chunks: bad view size");
+    // The kernel maps one wave64 to one pixel's samples: 32x32 threads / ppc
+    // must be 64, i.e. chunk_w = 4 as in the reference (main.rs:602).
+    if (u->chunk_w != 4) return fail(c, MM_ERR_UNSUPPORTED, "mm_trace_chunks: chunk_w must be 4 (64 samples/pixel)");
+    const uint32_t ppc = 16;
+    const uint32_t gw = (uint32_t)(u->view_w / 2.0f / (float)ppc), gh = (uint32_t)(u->view_h / 2.0f / (float)ppc);
+    if (gw == 0 || gh == 0) return fail(c, MM_ERR_INVALID, "mm_trace_chunks: view too small for one group");
+    // every pixel_buffer_index the groups compute (in float, IR %26-%31) must be in range
+    uint32_t max_pbi = 0;
+    for (uint32_t gy = 0; gy < gh; ++gy) {
+        float f = ((u->view_w * 0.5f) * (float)gy) / (float)ppc + (float)(gw - 1);
+        max_pbi = std::max(max_pbi, (uint32_t)f);
+    }
+    if (max_pbi >= n_chunks) return fail(c, MM_ERR_INVALID, "mm_trace_chunks: chunk list shorter than the grid");
+    const uint32_t W = (uint32_t)u->view_w, H = (uint32_t)u->view_h;
+    HIPC(c, hipSetDevice(c->device));
+    if (W != c->fb_w || H != c->fb_h) {
+        (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8);
+        c->d_fb = nullptr; c->d_fb8 = nullptr;
+        HIPC(c, hipMalloc((void**)&c->d_fb, (size_t)W * H * sizeof(float4)));
+        HIPC(c, hipMalloc((void**)&c->d_fb8, (size_t)W * H * sizeof(uint32_t)));
+        HIPC(c, hipMemsetAsync(c->d_fb, 0, (size_t)W * H * sizeof(float4), c->stream));
+        HIPC(c, hipMemsetAsync(c->d_fb8, 0, (size_t)W * H * sizeof(uint32_t), c->stream));
+        c->fb_w = W; c->fb_h = H;
+    }
+    int rc = ensure(c, c->d_chunks, c->chunks_cap, 2 * (size_t)n_chunks);
+    if (rc) return rc;
+    HIPC(c, hipMemcpyAsync(c->d_chunks, chunks, 2 * (size_t)n_chunks * sizeof(uint32_t), hipMemcpyHostToDevice,
+                           c->stream));
+    HIPC(c, hipMemsetAsync(c->d_aux, 0, 8 * sizeof(unsigned long long), c->stream));
+    if ((rc = begin_timing(c))) return rc;
+    HIPC(c, launch_trace_chunks(dev_scene(c), *u, c->d_chunks, gw, gh, c->d_fb, c->d_fb8, c->d_aux,
+                                reinterpret_cast<uint32_t*>(c->d_aux + 4), false, c->stream));
+    if ((rc = end_timing(c, 1))) return rc;
+    return read_aux(c, nullptr);
+}
+
+int mm_read_framebuffer(mm_ctx* c, float* rgba, uint8_t* rgba8) {
+    if (!c) return MM_ERR_INVALID;
+    if (!c->d_fb) return fail(c, MM_ERR_INVALID, "mm_read_framebuffer: nothing rendered yet");
+    const size_t n = (size_t)c->fb_w * c->fb_h;
+    HIPC(c, hipSetDevice(c->device));
+    if (rgba) HIPC(c, hipMemcpyAsync(rgba, c->d_fb, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    if (rgba8) HIPC(c, hipMemcpyAsync(rgba8, c->d_fb8, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MM_OK;
+}
+
+int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, uint32_t y0, uint32_t w,
+                  uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
+    if (!c) return MM_ERR_INVALID;
+    if (!c->has_scene) return fail(c, MM_ERR_NO_SCENE, "mm_trace_tile: no scene uploaded");
+    if (!u || !e || !out_dev) return fail(c, MM_ERR_INVALID, "mm_trace_tile: null argument");
+    if (!(u->view_w >= 1.0f && u->view_w <= 65536.0f && u->view_h >= 1.0f && u->view_h <= 65536.0f))
+        return fail(c, MM_ERR_INVALID, "mm_trace_tile: bad view size");
+    const uint32_t W = (uint32_t)u->view_w, H = (uint32_t)u->view_h;
+    if (w == 0 || h == 0 || y_stride == 0 || e->spp == 0 || e->spp > 4096)
+        return fail(c, MM_ERR_INVALID, "mm_trace_tile: empty tile or bad spp");
+    if ((uint64_t)x0 + w > W || (uint64_t)y0 + (uint64_t)(h - 1) * y_stride >= H)
+        return fail(c, MM_ERR_INVALID, "mm_trace_tile: tile outside the frame");
+    HIPC(c, hipSetDevice(c->device));
+    const bool want_stats = (e->flags & MM_EXT_COUNT_STATS) != 0;
+    // Bound the per-sample staging buffer: process whole rows, <= 64 Mi paths.
+    const uint64_t row_paths = (uint64_t)w * e->spp;
+    const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, (64ull << 20) / row_paths));
+    if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
+    int rc = ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
+    if (rc) return rc;
+    HIPC(c, hipMemsetAsync(c->d_aux, 0, 8 * sizeof(unsigned long long), c->stream));
+    if ((rc = begin_timing(c))) return rc;
+    uint32_t launches = 0;
+    for (uint32_t j0 = 0; j0 < h; j0 += rows_per_batch) {
+        TileJob job;
+        job.u = *u;
+        job.e = *e;
+        job.x0 = x0;
+        job.y0 = y0 + j0 * y_stride;
+        job.w = w;
+        job.h = std::min(rows_per_batch, h - j0);
+        job.y_stride = y_stride;
+        job.view_w = W;
+        if ((rc = prof_mark(c))) return rc;
+        HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux,
+                                  reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, c->stream));
+        if ((rc = prof_mark(c))) return rc;
+        HIPC(c, launch_resolve(job, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
+        launches += 2;
+    }
+    if ((rc = end_timing(c, launches))) return rc;
+    if (want_stats) return read_aux(c, stats);
+    return MM_OK;
+}
+
+int mm_sync(mm_ctx* c) {
+    if (!c) return MM_ERR_INVALID;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return read_aux(c, nullptr);
+}
+
+int mm_set_profiling(mm_ctx* c, int enable) {
+    if (!c) return MM_ERR_INVALID;
+    c->prof = enable != 0;
+    return MM_OK;
+}
+
+int mm_kernel_timing(mm_ctx* c, float* total_ms, uint32_t* launches, int reset) {
+    if (!c) return MM_ERR_INVALID;
+    HIPC(c, hipSetDevice(c->device));
+    float sum = 0.0f;
+    for (size_t i = 0; i + 1 < c->prof_used; i += 2) {
+        float ms = 0.0f;
+        HIPC(c, hipEventSynchronize(c->prof_ev[i + 1]));
+        HIPC(c, hipEventElapsedTime(&ms, c->prof_ev[i], c->prof_ev[i + 1]));
+        sum += ms;
+    }
+    if (total_ms) *total_ms = sum;
+    if (launches) *launches = (uint32_t)(c->prof_used / 2);
+    if (reset) c->prof_used = 0;
+    return MM_OK;
+}
+
+int mm_last_timing(mm_ctx* c, float* ms, uint32_t* launches) {
+    if (!c) return MM_ERR_INVALID;
+    if (c->last_ms < 0.0f) {
+        HIPC(c, hipEventSynchronize(c->ev1));
+        HIPC(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    }
+    if (ms) *ms = c->last_ms;
+    if (launches) *launches = c->last_launches;
+    return MM_OK;
+}
+
+}  // extern "C"

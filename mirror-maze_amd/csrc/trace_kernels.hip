@@ -1,0 +1,184 @@
+// trace_kernels.hip — gfx950 kernels for mirror-maze's per-pixel ray-trace loop.
+//
+//   k_prep_rects      per-rect subexpressions of ray_rect_intersect
+//   k_trace_chunks    parity mode: the reference dispatch (shaders.metal:245-368)
+//   k_trace_mega      throughput mode, one thread per (pixel, sample) path
+//   k_resolve         per-pixel sample reduction in the reference's order
+#include <hip/hip_runtime.h>
+
+#include "mm_launch.h"
+#include "mm_trace.h"
+
+namespace mm {
+
+// ---------------------------------------------------------------------------
+__global__ void k_prep_rects(const mm_rect* __restrict__ rects, uint32_t n, float4* __restrict__ geo) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const mm_rect r = rects[k];
+    const F3 o = F3{r.o[0], r.o[1], r.o[2]};
+    const F3 v = F3{r.v[0], r.v[1], r.v[2]};
+    const F3 u = F3{r.u[0], r.u[1], r.u[2]};
+    const F3 nn = normalize3(cross3(v, u));       // shaders.metal:52 (and :309)
+    const float lv = sqrtf(dot3(v, v));           // length(mirror.v), :60
+    const float lu = sqrtf(dot3(u, u));           // length(mirror.u), :61
+    geo[4 * k + 0] = make_float4(o.x, o.y, o.z, lv);
+    geo[4 * k + 1] = make_float4(nn.x, nn.y, nn.z, lu);
+    geo[4 * k + 2] = make_float4(v.x, v.y, v.z, 0.0f);
+    geo[4 * k + 3] = make_float4(u.x, u.y, u.z, 0.0f);
+}
+
+hipError_t launch_prep_rects(const mm_rect* rects_dev, uint32_t n, float4* geo_dev, hipStream_t s) {
+    hipLaunchKernelGGL(k_prep_rects, dim3((n + 255) / 256), dim3(256), 0, s, rects_dev, n, geo_dev);
+    return hipGetLastError();
+}
+
+// Sum per-thread counters over the wave, one atomic per wave.
+__device__ __forceinline__ void flush_stats(unsigned long long* stats, const Counters& c, uint32_t paths) {
+    unsigned long long v[4] = {c.rays, c.visits, c.rtests, paths};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        unsigned long long x = v[i];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        v[i] = x;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&stats[0], v[0]);
+        atomicAdd(&stats[1], v[1]);
+        atomicAdd(&stats[2], v[2]);
+        atomicAdd(&stats[3], v[3]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Parity mode.  One workgroup = one reference threadgroup of 32x32 threads;
+// flat = gid.x + 32*gid.y, so each wave64 holds exactly the 64 samples of one
+// pixel (pixel_number = flat/64, shaders.metal:271-275) and the reference's
+// threadgroup-memory tree reduction (shaders.metal:342-367) becomes a
+// shuffle reduction inside the wave with the same pairing and order.
+template <bool kStats>
+__global__ __launch_bounds__(1024) void k_trace_chunks(DevScene sc, mm_uniform u,
+                                                       const uint32_t* __restrict__ chunks, float4* __restrict__ fb,
+                                                       uint32_t* __restrict__ fb8, unsigned long long* stats,
+                                                       uint32_t* err) {
+    const uint32_t W = (uint32_t)u.view_w, H = (uint32_t)u.view_h;
+    const uint32_t chunk = u.chunk_w, ppc = chunk * chunk;  // 4, 16
+    const uint32_t gx = blockIdx.x, gy = blockIdx.y;
+    // pixel_buffer_index in float, IR %26-%31
+    const uint32_t pbi = cvt_u32_sat(((u.view_w * 0.5f) * (float)gy) / (float)ppc + (float)gx);
+    const uint32_t cx = chunks[2 * pbi], cy = chunks[2 * pbi + 1];
+    const uint32_t flat = threadIdx.x;          // 0..1023
+    const uint32_t lx = flat & 31, ly = flat >> 5;
+    const uint32_t pn = flat >> 6;              // flat / (1024 / 16)
+    const uint32_t px = cx + pn / chunk, py = cy + pn % chunk;
+    uint32_t seed = seed_reference(gx * 32 + lx, gy * 32 + ly, u.time);
+    const F3 d = jitter(primary_dir(u, px, py), seed);
+    const F3 ori = F3{u.cam.center[0], u.cam.center[1], u.cam.center[2]};
+    uint32_t stack[kStackMax];
+    Counters c;
+    bool overflow = false;
+    F3 s = trace_path<kStats>(sc, ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
+    if (overflow) atomicOr(err, 1u);
+    // level 1..3: test[f] += test[f+1], += test[f+2], += test[f+4]
+    s = s + F3{__shfl_xor(s.x, 1), __shfl_xor(s.y, 1), __shfl_xor(s.z, 1)};
+    s = s + F3{__shfl_xor(s.x, 2), __shfl_xor(s.y, 2), __shfl_xor(s.z, 2)};
+    s = s + F3{__shfl_xor(s.x, 4), __shfl_xor(s.y, 4), __shfl_xor(s.z, 4)};
+    // first thread of the pixel: acc = blk0 + blk1 + ... + blk7, then / 64
+    F3 acc = s;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) acc = acc + F3{__shfl(s.x, 8 * i), __shfl(s.y, 8 * i), __shfl(s.z, 8 * i)};
+    if (kStats) flush_stats(stats, c, 64);
+    if ((flat & 63) == 0 && px < W && py < H) {
+        const float m = 64.0f;
+        const F3 o = F3{acc.x / m, acc.y / m, acc.z / m};
+        fb[(size_t)py * W + px] = make_float4(o.x, o.y, o.z, 1.0f);
+        fb8[(size_t)py * W + px] = unorm8(o.x) | (unorm8(o.y) << 8) | (unorm8(o.z) << 16) | (255u << 24);
+    }
+}
+
+hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const uint32_t* chunks_dev,
+                               uint32_t grid_w, uint32_t grid_h, float4* fb, uint32_t* fb8,
+                               unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s) {
+    if (count_stats)
+        hipLaunchKernelGGL(k_trace_chunks<true>, dim3(grid_w, grid_h), dim3(1024), 0, s, sc, u, chunks_dev, fb, fb8,
+                           stats_dev, err);
+    else
+        hipLaunchKernelGGL(k_trace_chunks<false>, dim3(grid_w, grid_h), dim3(1024), 0, s, sc, u, chunks_dev, fb, fb8,
+                           stats_dev, err);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Throughput mode megakernel: path = pixel*spp + sample.
+template <bool kStats>
+__global__ __launch_bounds__(256) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                    unsigned long long* stats, uint32_t* err) {
+    const uint32_t spp = job.e.spp;
+    const uint32_t n_paths = job.w * job.h * spp;
+    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
+    Counters c;
+    if (path < n_paths) {
+        const uint32_t pix = path / spp, smp = path - pix * spp;
+        const uint32_t j = pix / job.w, i = pix - j * job.w;
+        const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
+        uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
+        const F3 d = jitter(primary_dir(job.u, px, py), seed);
+        const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
+        uint32_t stack[kStackMax];
+        bool overflow = false;
+        const F3 s = trace_path<kStats>(sc, ori, d, seed, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack,
+                                        c, overflow);
+        if (overflow) atomicOr(err, 1u);
+        samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
+    }
+    if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
+}
+
+hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats_dev,
+                             uint32_t* err, bool count_stats, hipStream_t s) {
+    const uint32_t n = job.w * job.h * job.e.spp;
+    const dim3 grid((n + 255) / 256);
+    if (count_stats)
+        hipLaunchKernelGGL(k_trace_mega<true>, grid, dim3(256), 0, s, sc, job, samples, stats_dev, err);
+    else
+        hipLaunchKernelGGL(k_trace_mega<false>, grid, dim3(256), 0, s, sc, job, samples, stats_dev, err);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Sample reduction: spp % 8 == 0 -> pairwise tree in blocks of 8, blocks added
+// left to right (the reference order for 64 spp); otherwise left to right.
+__global__ void k_resolve(TileJob job, const float4* __restrict__ samples, float4* __restrict__ out) {
+    const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= job.w * job.h) return;
+    const uint32_t spp = job.e.spp;
+    const float4* s = samples + (size_t)pix * spp;
+    F3 acc;
+    if (spp % 8 == 0) {
+        for (uint32_t b = 0; b < spp; b += 8) {
+            const F3 p0 = xyz(s[b + 0]) + xyz(s[b + 1]), p1 = xyz(s[b + 2]) + xyz(s[b + 3]);
+            const F3 p2 = xyz(s[b + 4]) + xyz(s[b + 5]), p3 = xyz(s[b + 6]) + xyz(s[b + 7]);
+            const F3 blk = (p0 + p1) + (p2 + p3);
+            acc = (b == 0) ? blk : acc + blk;
+        }
+    } else {
+        acc = xyz(s[0]);
+        for (uint32_t k = 1; k < spp; ++k) acc = acc + xyz(s[k]);
+    }
+    const float m = (float)spp;
+    const F3 v = F3{acc.x / m, acc.y / m, acc.z / m};
+    if (job.e.flags & MM_EXT_ACCUMULATE) {
+        float4 o = out[pix];
+        out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
+    } else {
+        out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
+    }
+}
+
+hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s) {
+    const uint32_t n = job.w * job.h;
+    hipLaunchKernelGGL(k_resolve, dim3((n + 255) / 256), dim3(256), 0, s, job, samples, out);
+    return hipGetLastError();
+}
+
+}  // namespace mm

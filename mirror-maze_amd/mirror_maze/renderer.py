@@ -1,0 +1,126 @@
+"""Renderer: the reference's compute dispatch as a Python object over the C ABI.
+
+Method names follow the reference's operator interface:
+  * ``upload_scene``   — make_buf for buffers 1, 2, 3, 5, 6 (src/main.rs:725-730)
+  * ``compute_shader`` — copy_to_buf(chunks) + dispatch_thread_groups
+                         (src/main.rs:778-885, kernel src/shaders.metal:245-368)
+  * ``read_texture``   — the screen texture the dispatch writes
+  * ``trace_tile``     — the offline renderer's throughput entry point
+
+Device buffers for ``trace_tile`` are torch tensors on the GPU (torch is the
+device-memory/stream plumbing); the library enqueues on torch's current
+stream so ordering with torch ops (e.g. an RCCL gather) is preserved.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .scene import Scene
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self._ctx = C.c_void_p()
+        check(lib().mm_create(device, C.byref(self._ctx)))
+        self.device = device
+        self._view = None
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            lib().mm_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> None:
+        check(rc, self._ctx)
+
+    def set_stream(self, stream=None) -> None:
+        """Enqueue on a torch.cuda.Stream (or raw hipStream_t int); None = own stream."""
+        handle = None if stream is None else int(getattr(stream, "cuda_stream", stream))
+        self._check(lib().mm_set_stream(self._ctx, handle))
+
+    def set_pipeline(self, pipe: int) -> None:
+        self._check(lib().mm_set_pipeline(self._ctx, pipe))
+
+    # -- scene ------------------------------------------------------------
+    def upload_scene(self, s: Scene) -> None:
+        rects = np.ascontiguousarray(s.rects, dtype=np.float32)
+        nodes = np.ascontiguousarray(s.nodes)
+        idx = np.ascontiguousarray(s.idx, dtype=np.uint32)
+        mats = np.ascontiguousarray(s.is_mirror, dtype=np.uint8)
+        emis = np.ascontiguousarray(s.emission, dtype=np.float32)
+        self._check(lib().mm_upload_scene(self._ctx, rects.ctypes.data, rects.shape[0], nodes.ctypes.data,
+                                          nodes.shape[0], idx.ctypes.data, mats.ctypes.data, emis.ctypes.data))
+
+    # -- parity mode --------------------------------------------------------
+    def compute_shader(self, uniform: _lib.mm_uniform, pixel_update_buffer: np.ndarray) -> None:
+        """One reference dispatch: (W/32)x(H/32) groups, 64 samples per pixel."""
+        chunks = np.ascontiguousarray(pixel_update_buffer, dtype=np.uint32).reshape(-1, 2)
+        self._check(lib().mm_trace_chunks(self._ctx, C.byref(uniform), chunks.ctypes.data, chunks.shape[0]))
+        self._view = (int(uniform.view_w), int(uniform.view_h))
+
+    def read_texture(self):
+        """(rgba_f32 [H,W,4], rgba8 [H,W,4]) of the screen texture."""
+        if self._view is None:
+            raise RuntimeError("nothing rendered yet")
+        W, H = self._view
+        f = np.zeros((H, W, 4), dtype=np.float32)
+        b = np.zeros((H, W, 4), dtype=np.uint8)
+        self._check(lib().mm_read_framebuffer(self._ctx, f.ctypes.data, b.ctypes.data))
+        return f, b
+
+    # -- throughput mode ------------------------------------------------------
+    def trace_tile(self, uniform: _lib.mm_uniform, ext: _lib.mm_ext, x0: int, y0: int, w: int, h: int,
+                   y_stride: int = 1, out=None, stats: bool = False):
+        """Render a tile into a (h, w, 4) float32 CUDA tensor (allocated if None).
+        Returns (out, mm_stats or None)."""
+        import torch
+
+        if out is None:
+            out = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{self.device}")
+        if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous() and out.numel() == h * w * 4):
+            raise ValueError("out must be a contiguous float32 CUDA tensor of h*w*4 elements")
+        e = _lib.mm_ext(ext.spp, ext.bounce_limit, ext.mirror_limit, ext.frame,
+                        ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0), 0)
+        st = _lib.mm_stats()
+        self._check(lib().mm_trace_tile(self._ctx, C.byref(uniform), C.byref(e), x0, y0, w, h, y_stride,
+                                        out.data_ptr(), C.byref(st)))
+        return out, (st if stats else None)
+
+    def sync(self) -> None:
+        self._check(lib().mm_sync(self._ctx))
+
+    def set_profiling(self, enable: bool = True) -> None:
+        self._check(lib().mm_set_profiling(self._ctx, 1 if enable else 0))
+
+    def kernel_timing(self, reset: bool = True):
+        """(summed ms, launches) of the ray-trace kernel since the last reset."""
+        ms, n = C.c_float(), C.c_uint32()
+        self._check(lib().mm_kernel_timing(self._ctx, C.byref(ms), C.byref(n), 1 if reset else 0))
+        return ms.value, n.value
+
+    def last_timing(self):
+        ms, n = C.c_float(), C.c_uint32()
+        self._check(lib().mm_last_timing(self._ctx, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+def make_ext(spp: int = 8, bounce_limit: int = 8, mirror_limit: int = 8, frame: int = 0,
+             flags: int = 0) -> _lib.mm_ext:
+    return _lib.mm_ext(spp, bounce_limit, mirror_limit, frame, flags, 0)

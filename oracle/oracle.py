@@ -1,0 +1,126 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle
+(oracle/_build/libmm_oracle.so, a restatement of src/shaders.metal:245-368).
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg; never from the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "libmm_oracle.so"
+
+
+class _U(C.Structure):  # mm_uniform, include/mm_types.h
+    _fields_ = [("center", C.c_float * 3), ("focal", C.c_float), ("quat", C.c_float * 4),
+                ("viewport", C.c_float * 2), ("view_w", C.c_float), ("view_h", C.c_float),
+                ("chunk_w", C.c_uint32), ("time", C.c_uint32)]
+
+
+class OracleScene(C.Structure):
+    _fields_ = [("rects", C.c_void_p), ("n_rects", C.c_uint32), ("nodes", C.c_void_p), ("n_nodes", C.c_uint32),
+                ("idx", C.c_void_p), ("is_mirror", C.c_void_p), ("emission", C.c_void_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("rect_tests", C.c_uint64), ("paths", C.c_uint64)]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        P = C.c_void_p
+        L.oracle_trace_chunks.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+        L.oracle_trace_group.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+        L.oracle_trace_tile.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+        L.oracle_trace_path.argtypes = [P, P, P, C.c_uint32, C.c_int, C.c_int, P, P]
+        L.oracle_rand_pm1.argtypes = [P]
+        L.oracle_rand_pm1.restype = C.c_float
+        L.oracle_seed_reference.argtypes = [C.c_uint32] * 3
+        L.oracle_seed_reference.restype = C.c_uint32
+        L.oracle_tile_seed.argtypes = [C.c_uint32] * 3
+        L.oracle_tile_seed.restype = C.c_uint32
+        L.oracle_primary_dir.argtypes = [P, C.c_uint32, C.c_uint32, P]
+        L.oracle_intersect_aabb.argtypes = [P, P, C.c_float, P, P]
+        L.oracle_intersect_aabb.restype = C.c_float
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    """Holds numpy copies of a scene and calls the oracle on them."""
+
+    def __init__(self, rects, nodes, idx, is_mirror, emission):
+        self.rects = np.ascontiguousarray(rects, dtype=np.float32)
+        self.nodes = np.ascontiguousarray(nodes)
+        self.idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        self.is_mirror = np.ascontiguousarray(is_mirror, dtype=np.uint8)
+        self.emission = np.ascontiguousarray(emission, dtype=np.float32)
+        self.sc = OracleScene(self.rects.ctypes.data, self.rects.shape[0], self.nodes.ctypes.data,
+                              self.nodes.shape[0], self.idx.ctypes.data, self.is_mirror.ctypes.data,
+                              self.emission.ctypes.data)
+
+    @classmethod
+    def from_scene(cls, s) -> "Oracle":
+        return cls(s.rects, s.nodes, s.idx, s.is_mirror, s.emission)
+
+    @staticmethod
+    def _u(uniform) -> bytes:
+        return bytes(uniform)  # mm_uniform is 56 B, same layout
+
+    def trace_chunks(self, uniform, chunks, fb=None, tg=(32, 32)):
+        W, H = int(uniform.view_w), int(uniform.view_h)
+        if fb is None:
+            fb = np.zeros((H, W, 4), dtype=np.float32)
+        ch = np.ascontiguousarray(chunks, dtype=np.uint32).reshape(-1, 2)
+        ub = C.create_string_buffer(bytes(uniform), len(bytes(uniform)))
+        st = Stats()
+        rc = lib().oracle_trace_chunks(C.byref(self.sc), ub, ch.ctypes.data, ch.shape[0], tg[0], tg[1],
+                                       fb.ctypes.data, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle_trace_chunks rc={rc}")
+        return fb, st
+
+    def trace_group(self, uniform, chunks, gx, gy, fb, tg=(32, 32)):
+        ch = np.ascontiguousarray(chunks, dtype=np.uint32).reshape(-1, 2)
+        ub = C.create_string_buffer(bytes(uniform), len(bytes(uniform)))
+        st = Stats()
+        rc = lib().oracle_trace_group(C.byref(self.sc), ub, ch.ctypes.data, ch.shape[0], tg[0], tg[1], gx, gy,
+                                      fb.ctypes.data, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle_trace_group rc={rc}")
+        return st
+
+    def trace_tile(self, uniform, ext, x0, y0, w, h, y_stride=1, out=None):
+        if out is None:
+            out = np.zeros((h, w, 4), dtype=np.float32)
+        ub = C.create_string_buffer(bytes(uniform), len(bytes(uniform)))
+        eb = C.create_string_buffer(bytes(ext), len(bytes(ext)))
+        st = Stats()
+        rc = lib().oracle_trace_tile(C.byref(self.sc), ub, eb, x0, y0, w, h, y_stride, out.ctypes.data, C.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle_trace_tile rc={rc}")
+        return out, st
+
+    def trace_path(self, ori, d, seed, bounce_limit=5, mirror_limit=15):
+        o = np.asarray(ori, dtype=np.float32)
+        dd = np.asarray(d, dtype=np.float32)
+        rgb = np.zeros(3, dtype=np.float32)
+        rays = C.c_uint32()
+        rc = lib().oracle_trace_path(C.byref(self.sc), o.ctypes.data, dd.ctypes.data, seed, bounce_limit,
+                                     mirror_limit, rgb.ctypes.data, C.byref(rays))
+        return rgb, rays.value, rc

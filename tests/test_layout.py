@@ -1,0 +1,73 @@
+"""C-ABI boundary: struct layouts and exported symbols (CPU, no compute calls)."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+import subprocess
+
+from conftest import PKG, REPO
+
+
+def test_struct_sizes_match_reference_repr_c():
+    from mirror_maze import _lib
+
+    # Plane / BVHNode / Camera / Uniform of src/main.rs:32-81
+    assert C.sizeof(_lib.mm_rect) == 48
+    assert C.sizeof(_lib.mm_node) == 32
+    assert C.sizeof(_lib.mm_camera) == 40
+    assert C.sizeof(_lib.mm_uniform) == 56
+    assert _lib.mm_uniform.view_w.offset == 40 and _lib.mm_uniform.time.offset == 52
+    assert _lib.mm_node.left_first.offset == 24 and _lib.mm_node.count.offset == 28
+    assert C.sizeof(_lib.mm_ext) == 24 and C.sizeof(_lib.mm_stats) == 32
+
+
+def _declared_functions():
+    names = set()
+    for h in ("mm_api.h", "mm_scene.h"):
+        txt = (REPO / "include" / h).read_text()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s+\**\s*(mm_[a-z_0-9]+)\s*\(", txt, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    from mirror_maze import _lib
+
+    lib = _lib.lib()
+    declared = _declared_functions()
+    assert len(declared) >= 25, declared
+    missing = [n for n in sorted(declared) if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python binding covers exactly the declared surface
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    assert lib.mm_version().startswith(b"mirror-maze-amd")
+
+
+def test_shared_object_is_gfx950_code():
+    so = PKG / "lib" / "libmirror_maze.so"
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", str(so)], capture_output=True, text=True)
+    if out.returncode != 0:  # tool absent: fall back to the offload bundle marker
+        data = so.read_bytes()
+        assert b"gfx950" in data
+    else:
+        assert "gfx950" in out.stdout
+
+
+def test_layout_static_asserts_compiled():
+    from mirror_maze import _lib
+
+    assert _lib.lib().mm_layout_ok() == 1
+
+
+def test_errors_are_codes_not_crashes():
+    """Calls that need no GPU must return codes, never abort."""
+    from mirror_maze import _lib
+
+    L = _lib.lib()
+    assert L.mm_create(0, None) == _lib.MM_ERR_INVALID
+    assert L.mm_set_stream(None, None) == _lib.MM_ERR_INVALID
+    assert L.mm_upload_scene(None, None, 0, None, 0, None, None, None) == _lib.MM_ERR_INVALID
+    assert L.mm_trace_chunks(None, None, None, 0) == _lib.MM_ERR_INVALID
+    assert L.mm_sync(None) == _lib.MM_ERR_INVALID
+    assert L.mm_last_error(None) == b"null context"
