@@ -40,7 +40,9 @@ void mm_destroy(mm_ctx* ctx);
 const char* mm_last_error(const mm_ctx* ctx);
 
 /* Enqueue on a caller stream (hipStream_t passed as void*), e.g. torch's
- * current stream; NULL restores the context's own stream. */
+ * current stream.  NULL is HIP's default (null) stream, as in HIP itself;
+ * MM_OWN_STREAM restores the context's own non-blocking stream. */
+#define MM_OWN_STREAM ((void*)(intptr_t)-1)
 int  mm_set_stream(mm_ctx* ctx, void* hip_stream);
 
 /* Replaces make_buf for buffers 1,2,3,5,6 (main.rs:725-730):

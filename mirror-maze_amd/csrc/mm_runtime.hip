@@ -207,7 +207,7 @@ const char* mm_last_error(const mm_ctx* c) { return c ? c->err.c_str() : "null c
 
 int mm_set_stream(mm_ctx* c, void* s) {
     if (!c) return MM_ERR_INVALID;
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = (s == MM_OWN_STREAM) ? c->own_stream : (hipStream_t)s;
     return MM_OK;
 }
 

@@ -28,6 +28,7 @@ class Renderer:
         check(lib().mm_create(device, C.byref(self._ctx)))
         self.device = device
         self._view = None
+        self._pinned_stream = False
 
     # -- lifecycle --------------------------------------------------------
     def close(self) -> None:
@@ -51,8 +52,10 @@ class Renderer:
         check(rc, self._ctx)
 
     def set_stream(self, stream=None) -> None:
-        """Enqueue on a torch.cuda.Stream (or raw hipStream_t int); None = own stream."""
-        handle = None if stream is None else int(getattr(stream, "cuda_stream", stream))
+        """Pin a torch.cuda.Stream (or raw hipStream_t int).  None = follow
+        torch's current stream at every trace_tile call (the default)."""
+        self._pinned_stream = stream is not None
+        handle = _lib.MM_OWN_STREAM if stream is None else int(getattr(stream, "cuda_stream", stream))
         self._check(lib().mm_set_stream(self._ctx, handle))
 
     def set_pipeline(self, pipe: int) -> None:
@@ -96,6 +99,8 @@ class Renderer:
             out = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{self.device}")
         if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous() and out.numel() == h * w * 4):
             raise ValueError("out must be a contiguous float32 CUDA tensor of h*w*4 elements")
+        if not self._pinned_stream:  # order with the torch ops that made / read `out`
+            self._check(lib().mm_set_stream(self._ctx, torch.cuda.current_stream(out.device).cuda_stream))
         e = _lib.mm_ext(ext.spp, ext.bounce_limit, ext.mirror_limit, ext.frame,
                         ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0), 0)
         st = _lib.mm_stats()
