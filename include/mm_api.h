@@ -92,7 +92,14 @@ int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
 #define MM_PIPE_AUTO       0
 #define MM_PIPE_MEGAKERNEL 1   /* one thread per path, bounce loop in-kernel */
 #define MM_PIPE_WAVEFRONT  2   /* SoA path state + compacted ray queues      */
+#define MM_PIPE_REFERENCE  3   /* straight statement of the reference kernel
+                                  (IEEE division everywhere); A/B baseline  */
 int  mm_set_pipeline(mm_ctx* ctx, int pipe);
+
+/* Tuning knobs (results never change; only speed does). */
+#define MM_OPT_LDS_NODES   1   /* 1: stage the BVH in LDS when it fits (default), 0: read via L1/L2 */
+#define MM_OPT_BLOCK       2   /* threads per workgroup for the megakernel (64..1024, multiple of 64) */
+int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Wait for all work queued by this context. */
 int  mm_sync(mm_ctx* ctx);

@@ -17,23 +17,27 @@ constexpr float kBig = 1e30f;     // shaders.metal:15, 94, 149 (IR 0x46293E59400
 constexpr int kStackMax = 50;     // shaders.metal:123
 
 // ---- HBM layouts ------------------------------------------------------------
-// Node: 2 x float4 = the reference's 32-B bvh_node, re-typed for 16-B loads:
+// Reference node (nodes_ref): 2 x float4 = the reference's 32-B bvh_node,
 //   a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(left_first), bits(count))
+// Production node (nodes): same a; b = (mx.y, mx.z, bits(count<<24 | left_first), 0).
 // Children of an interior node are adjacent (left_first, left_first+1), so the
 // pair a traversal step reads is one contiguous 64-B line.
 //
 // Rect geometry: 4 x float4 per rect (64 B):
-//   g0 = (o.xyz, |v|)  g1 = (n.xyz, |u|)  g2 = (v.xyz, kind)  g3 = (u.xyz, 0)
+//   g0 = (o.xyz, |v|)  g1 = (n.xyz, |u|)  g2 = (v.xyz, 1/|v|)  g3 = (u.xyz, 1/|u|)
 // n, |v|, |u| are the per-rect subexpressions of ray_rect_intersect
 // (shaders.metal:52,60,61), computed once by k_prep_rects with the same ops.
 // Shade record: s0 = (color.rgb, is_mirror), s1 = emission (rgba).
 struct DevScene {
-    const float4* nodes;      // 2 * n_nodes
+    const float4* nodes;      // 2 * n_nodes, production layout
+    const float4* nodes_ref;  // 2 * n_nodes, reference layout
     const float4* geo;        // 4 * n_rects
     const float4* shade;      // 2 * n_rects
     const uint32_t* idx;      // n_rects
     uint32_t n_nodes;
     uint32_t n_rects;
+    uint32_t root_packed;     // count<<24 | left_first of node 0
+    uint32_t fast_ok;         // scene coordinates inside the Markstein guard
 };
 
 // ---- IEEE helpers (the AIR intrinsics with their IEEE meaning) -------------

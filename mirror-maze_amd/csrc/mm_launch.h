@@ -22,10 +22,17 @@ struct TileJob {
     uint32_t view_w;     // (uint32_t)u.view_w — pixel index stride
 };
 
+struct MegaOpts {
+    bool reference = false;   // traverse_reference (IEEE division), A/B baseline
+    bool lds_nodes = false;   // stage nodes in LDS
+    uint32_t block = 256;     // threads per workgroup
+};
+
 // Throughput mode, megakernel: one thread per (pixel, sample) path; writes
 // the per-sample value sqrt(max(L,0)) to samples[path] (path = pixel*spp+s).
 hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples,
-                             unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
+                             unsigned long long* stats_dev, uint32_t* err, bool count_stats,
+                             const MegaOpts& o, hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);

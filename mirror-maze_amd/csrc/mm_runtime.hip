@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -26,7 +27,10 @@ struct mm_ctx {
     std::string err;
     // scene (buffers 1,2,3,5,6 of compute_shader)
     mm_rect* d_rects = nullptr;
-    float4* d_nodes = nullptr;
+    float4* d_nodes = nullptr;      // production layout (packed child words)
+    float4* d_nodes_ref = nullptr;  // reference layout
+    uint32_t root_packed = 0;
+    bool fast_ok = false;
     float4* d_geo = nullptr;
     float4* d_shade = nullptr;
     uint32_t* d_idx = nullptr;
@@ -48,6 +52,8 @@ struct mm_ctx {
     float last_ms = 0.0f;
     uint32_t last_launches = 0;
     int pipe = MM_PIPE_AUTO;
+    bool opt_lds = true;
+    uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
     // per-kernel profiling of the trace kernel (mm_set_profiling)
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
@@ -80,6 +86,9 @@ int ensure(mm_ctx* c, T*& ptr, size_t& cap, size_t n) {
 DevScene dev_scene(const mm_ctx* c) {
     DevScene s;
     s.nodes = c->d_nodes;
+    s.nodes_ref = c->d_nodes_ref;
+    s.root_packed = c->root_packed;
+    s.fast_ok = c->fast_ok ? 1u : 0u;
     s.geo = c->d_geo;
     s.shade = c->d_shade;
     s.idx = c->d_idx;
@@ -89,9 +98,9 @@ DevScene dev_scene(const mm_ctx* c) {
 }
 
 void free_scene(mm_ctx* c) {
-    (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_geo);
+    (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_nodes_ref); (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx);
-    c->d_rects = nullptr; c->d_nodes = nullptr; c->d_geo = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
+    c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
     c->has_scene = false;
 }
 
@@ -120,6 +129,17 @@ int check_tree(const mm_node* nodes, uint32_t n_nodes, const uint32_t* idx, uint
     }
     if (maxd > (uint32_t)kStackMax) { why = "BVH deeper than the 50-entry traversal stack"; return MM_ERR_STACK; }
     return MM_OK;
+}
+
+// Coordinates inside the Markstein-quotient guard (mm_trace.h): 0 or
+// |x| in [2^-30, 2^60]; rect extents 0 or |x| in [2^-10, 2^60].
+bool coord_ok(float x) {
+    const float a = std::fabs(x);
+    return a == 0.0f || (a >= 0x1p-30f && a <= 0x1p60f);
+}
+bool extent_ok(float x) {
+    const float a = std::fabs(x);
+    return a == 0.0f || (a >= 0x1p-10f && a <= 0x1p60f);
 }
 
 int begin_timing(mm_ctx* c) {
@@ -212,9 +232,22 @@ int mm_set_stream(mm_ctx* c, void* s) {
 }
 
 int mm_set_pipeline(mm_ctx* c, int pipe) {
-    if (!c || pipe < MM_PIPE_AUTO || pipe > MM_PIPE_WAVEFRONT) return MM_ERR_INVALID;
+    if (!c) return MM_ERR_INVALID;
+    if (pipe < MM_PIPE_AUTO || pipe > MM_PIPE_REFERENCE) return fail(c, MM_ERR_INVALID, "unknown pipeline");
     c->pipe = pipe;
     return MM_OK;
+}
+
+int mm_set_option(mm_ctx* c, int key, int value) {
+    if (!c) return MM_ERR_INVALID;
+    switch (key) {
+        case MM_OPT_LDS_NODES: c->opt_lds = value != 0; return MM_OK;
+        case MM_OPT_BLOCK:
+            if (value < 64 || value > 1024 || value % 64) return fail(c, MM_ERR_INVALID, "block must be 64..1024, x64");
+            c->opt_block = (uint32_t)value;
+            return MM_OK;
+        default: return fail(c, MM_ERR_INVALID, "unknown option");
+    }
 }
 
 int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
@@ -226,6 +259,20 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     std::string why;
     int rc = check_tree(nodes, n_nodes, idx, n_rects, why);
     if (rc != MM_OK) return fail(c, rc, "mm_upload_scene: " + why);
+    // production node layout: b.z = count << 24 | left_first
+    std::vector<mm_node> packed(nodes, nodes + n_nodes);
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+        if (nodes[i].count >= 256u || nodes[i].left_first >= (1u << 24))
+            return fail(c, MM_ERR_UNSUPPORTED, "mm_upload_scene: leaf with >= 256 planes or index >= 2^24");
+        packed[i].left_first = (nodes[i].count << 24) | nodes[i].left_first;
+        packed[i].count = 0;
+    }
+    bool fast = true;
+    for (uint32_t i = 0; i < n_nodes && fast; ++i)
+        for (int a = 0; a < 3; ++a) fast = fast && coord_ok(nodes[i].mn[a]) && coord_ok(nodes[i].mx[a]);
+    for (uint32_t k = 0; k < n_rects && fast; ++k)
+        for (int a = 0; a < 3; ++a)
+            fast = fast && coord_ok(rects[k].o[a]) && extent_ok(rects[k].v[a]) && extent_ok(rects[k].u[a]);
     HIPC(c, hipSetDevice(c->device));
     free_scene(c);
     std::vector<float4> shade(2 * (size_t)n_rects);
@@ -235,18 +282,22 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     }
     HIPC(c, hipMalloc((void**)&c->d_rects, n_rects * sizeof(mm_rect)));
     HIPC(c, hipMalloc((void**)&c->d_nodes, n_nodes * sizeof(mm_node)));
+    HIPC(c, hipMalloc((void**)&c->d_nodes_ref, n_nodes * sizeof(mm_node)));
     HIPC(c, hipMalloc((void**)&c->d_geo, 4 * (size_t)n_rects * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_shade, 2 * (size_t)n_rects * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_idx, n_rects * sizeof(uint32_t)));
     HIPC(c, hipMemcpyAsync(c->d_rects, rects, n_rects * sizeof(mm_rect), hipMemcpyHostToDevice, c->stream));
     // mm_node is exactly two float4: (mn.xyz, mx.x) (mx.yz, left_first, count)
-    HIPC(c, hipMemcpyAsync(c->d_nodes, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_nodes_ref, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_nodes, packed.data(), n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_idx, idx, n_rects * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));  // host arrays may be freed on return
     c->n_rects = n_rects;
     c->n_nodes = n_nodes;
+    c->root_packed = packed[0].left_first;
+    c->fast_ok = fast;
     c->has_scene = true;
     return MM_OK;
 }
@@ -338,8 +389,12 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         job.y_stride = y_stride;
         job.view_w = W;
         if ((rc = prof_mark(c))) return rc;
+        MegaOpts mo;
+        mo.reference = c->pipe == MM_PIPE_REFERENCE;
+        mo.lds_nodes = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
+        mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
         HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux,
-                                  reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, c->stream));
+                                  reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
         if ((rc = prof_mark(c))) return rc;
         HIPC(c, launch_resolve(job, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
         launches += 2;

@@ -1,8 +1,24 @@
 // mm_trace.h — the per-ray and per-path device code of the reference kernel:
 // ray_rect_intersect (shaders.metal:51-67), intersect_aabb (87-95),
 // intersect_bvh_iterative (115-156) and the bounce loop (302-340).
-// Operation order follows src/shaders.ir; see oracle/mm_oracle.c for the CPU
-// statement the parity tests compare against.
+// Operation order follows src/shaders.ir; oracle/mm_oracle.c is the CPU
+// statement the parity tests compare against, bit for bit.
+//
+// Two traversals are provided:
+//   traverse_reference  the straight statement (IEEE division everywhere);
+//                       kept as MM_PIPE_REFERENCE for A/B measurement.
+//   traverse<kFast>     the production path.  With kFast every slab division
+//                       (bound - o) / d uses a per-ray correctly rounded
+//                       reciprocal y = RN(1/d) and Markstein's correction
+//                           q = a*y;  r = fma(-q, d, a);  q' = fma(r, y, q)
+//                       which equals RN(a/d) when no under/overflow occurs
+//                       (Markstein 1990; Cornea-Hasegan, Golliver, Markstein
+//                       1999).  scripts/verify_markstein.c checks 1.6e9 pairs
+//                       over every divisor mantissa: 0 mismatches.  The
+//                       exponent ranges that theorem needs are enforced by
+//                       ray_fast_ok() per ray and by the scene check at upload;
+//                       a ray outside them takes traverse<false> (IEEE
+//                       division), so results are always the reference's.
 #pragma once
 
 #include "mm_device.h"
@@ -13,18 +29,59 @@ struct Counters {
     uint32_t rays = 0, visits = 0, rtests = 0;
 };
 
-// ray_rect_intersect with the per-rect subexpressions (n, |v|, |u|) loaded
-// from g0/g1 instead of recomputed (same IEEE ops, same values).
-__device__ __forceinline__ void rect_test(const float4* __restrict__ geo, uint32_t k, F3 ori, F3 dir,
-                                          float& t, uint32_t& index) {
+struct Ray {
+    F3 o, d;
+    F3 y;  // (1/d.x, 1/d.y, 1/d.z), IEEE division
+};
+
+__device__ __forceinline__ Ray make_ray(F3 o, F3 d) {
+    Ray r;
+    r.o = o;
+    r.d = d;
+    r.y = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    return r;
+}
+
+// Exponent guards for the Markstein quotient (see header comment).
+__device__ __forceinline__ bool dir_ok(float x) {
+    const float a = fabsf(x);
+    return a >= 0x1p-40f && a <= 0x1p40f;
+}
+__device__ __forceinline__ bool org_ok(float x) {
+    const float a = fabsf(x);
+    return a == 0.0f || (a >= 0x1p-30f && a <= 0x1p60f);
+}
+__device__ __forceinline__ bool ray_fast_ok(const Ray& r) {
+    return dir_ok(r.d.x) && dir_ok(r.d.y) && dir_ok(r.d.z) && org_ok(r.o.x) && org_ok(r.o.y) && org_ok(r.o.z);
+}
+
+// RN(a / d) given y = RN(1/d), inside the guarded ranges.
+__device__ __forceinline__ float qdiv(float a, float d, float y) {
+    const float q = a * y;
+    const float r = __builtin_fmaf(-q, d, a);
+    return __builtin_fmaf(r, y, q);
+}
+template <bool kFast>
+__device__ __forceinline__ float sdiv(float a, float d, float y) {
+    if constexpr (kFast) return qdiv(a, d, y);
+    else return a / d;
+}
+
+// ---------------------------------------------------------------------------
+// ray_rect_intersect.  g0 = (o, |v|), g1 = (n, |u|), g2 = (v, 1/|v|),
+// g3 = (u, 1/|u|): n, |v|, |u| are the reference's per-rect subexpressions
+// (same IEEE ops, computed once by k_prep_rects).
+template <bool kFast>
+__device__ __forceinline__ void rect_test(const float4* __restrict__ geo, uint32_t k, const Ray& r, float& t,
+                                          uint32_t& index) {
     const float4 g0 = geo[4 * k + 0], g1 = geo[4 * k + 1], g2 = geo[4 * k + 2], g3 = geo[4 * k + 3];
     const F3 o = xyz(g0), n = xyz(g1), v = xyz(g2), u = xyz(g3);
     const float lv = g0.w, lu = g1.w;
-    const float nc = dot3(dir, n);
-    const float a = dot3(o - ori, n) / nc;
-    const F3 rv = (ori - o) + a * dir;
-    const float d1 = dot3(rv, v) / lv;
-    const float d2 = dot3(rv, u) / lu;
+    const float nc = dot3(r.d, n);
+    const float a = dot3(o - r.o, n) / nc;
+    const F3 rv = (r.o - o) + a * r.d;
+    const float d1 = sdiv<kFast>(dot3(rv, v), lv, g2.w);
+    const float d2 = sdiv<kFast>(dot3(rv, u), lu, g3.w);
     if (d1 >= 0.0f && d1 <= lv && d2 >= 0.0f && d2 <= lu && nc != 0.0f && a > 0.1f && a < t) {
         t = a;
         index = k;
@@ -32,42 +89,87 @@ __device__ __forceinline__ void rect_test(const float4* __restrict__ geo, uint32
 }
 
 // intersect_aabb; a = (mn.xyz, mx.x), b = (mx.y, mx.z, ., .)
-__device__ __forceinline__ float aabb_test(float4 a, float4 b, F3 ori, F3 dir, float t) {
-    const float tx1 = (a.x - ori.x) / dir.x, tx2 = (a.w - ori.x) / dir.x;
+template <bool kFast>
+__device__ __forceinline__ float aabb_test(float4 a, float4 b, const Ray& r, float t) {
+    const float tx1 = sdiv<kFast>(a.x - r.o.x, r.d.x, r.y.x), tx2 = sdiv<kFast>(a.w - r.o.x, r.d.x, r.y.x);
     float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
-    const float ty1 = (a.y - ori.y) / dir.y, ty2 = (b.x - ori.y) / dir.y;
+    const float ty1 = sdiv<kFast>(a.y - r.o.y, r.d.y, r.y.y), ty2 = sdiv<kFast>(b.x - r.o.y, r.d.y, r.y.y);
     tmin = fmaxf(tmin, fminf(ty1, ty2));
     tmax = fminf(tmax, fmaxf(ty1, ty2));
-    const float tz1 = (a.z - ori.z) / dir.z, tz2 = (b.y - ori.z) / dir.z;
+    const float tz1 = sdiv<kFast>(a.z - r.o.z, r.d.z, r.y.z), tz2 = sdiv<kFast>(b.y - r.o.z, r.d.z, r.y.z);
     tmin = fmaxf(tmin, fminf(tz1, tz2));
     tmax = fminf(tmax, fmaxf(tz1, tz2));
     return (tmax >= tmin && tmin < t && tmax > 0.0f) ? tmin : kBig;
 }
 
-// intersect_bvh_iterative.  `stack` is any indexable storage of >= 50 u32.
-// Returns false on stack overflow (the reference would write out of bounds).
+// ---------------------------------------------------------------------------
+// intersect_bvh_iterative, production form.  Device node layout (built at
+// upload from the reference's 32-B BVHNode):
+//     a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(packed), 0)
+// packed = count << 24 | left_first.  Children are adjacent, so an interior
+// visit loads one 64-B pair and already holds each child's (lf, count): only
+// a pop needs no load at all because the stack holds packed words.  Visit
+// order, pruning and pushes are exactly the reference's.
+template <bool kFast, bool kStats, typename Nodes, typename Stack>
+__device__ __forceinline__ bool traverse(const DevScene& sc, const Nodes& nodes, const Ray& r, float& t,
+                                         uint32_t& index, Stack& stack, Counters& c) {
+    uint32_t cur = sc.root_packed, head = 0;
+    for (;;) {
+        const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+        if (cnt > 0) {
+            for (uint32_t i = 0; i < cnt; ++i) rect_test<kFast>(sc.geo, sc.idx[lf + i], r, t, index);
+            if (kStats) c.rtests += cnt;
+            if (head == 0) break;
+            cur = stack[--head];
+            continue;
+        }
+        if (kStats) c.visits++;
+        const float4 la = nodes[2 * lf], lb = nodes[2 * lf + 1], ra = nodes[2 * lf + 2], rb = nodes[2 * lf + 3];
+        float d1 = aabb_test<kFast>(la, lb, r, t);
+        float d2 = aabb_test<kFast>(ra, rb, r, t);
+        uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+        if (d1 > d2) {
+            const float tt = d1; d1 = d2; d2 = tt;
+            const uint32_t x = pl; pl = pr; pr = x;
+        }
+        if (d1 == kBig) {
+            if (head == 0) break;
+            cur = stack[--head];
+        } else {
+            cur = pl;
+            if (d2 != kBig) {
+                if (head >= (uint32_t)kStackMax) return false;
+                stack[head++] = pr;
+            }
+        }
+    }
+    return true;
+}
+
+// The straight statement of intersect_bvh_iterative over the reference node
+// layout (sc.nodes_ref, 2 float4 per node: a, (mx.yz, lf, count)).
 template <bool kStats, typename Stack>
-__device__ __forceinline__ bool intersect_bvh(const DevScene& sc, F3 ori, F3 dir, float& t, uint32_t& index,
-                                              Stack& stack, Counters& c) {
-    const float4* __restrict__ nodes = sc.nodes;
+__device__ __forceinline__ bool traverse_reference(const DevScene& sc, const Ray& r, float& t, uint32_t& index,
+                                                   Stack& stack, Counters& c) {
+    const float4* __restrict__ nodes = sc.nodes_ref;
     uint32_t node = 0, head = 0;
     for (;;) {
         const float4 nb = nodes[2 * node + 1];
         const uint32_t lf = __float_as_uint(nb.z), count = __float_as_uint(nb.w);
         if (count > 0) {
-            for (uint32_t i = 0; i < count; ++i) rect_test(sc.geo, sc.idx[lf + i], ori, dir, t, index);
+            for (uint32_t i = 0; i < count; ++i) rect_test<false>(sc.geo, sc.idx[lf + i], r, t, index);
             if (kStats) c.rtests += count;
             if (head == 0) break;
             node = stack[--head];
             continue;
         }
         if (kStats) c.visits++;
-        uint32_t l = lf, r = lf + 1;
-        float d1 = aabb_test(nodes[2 * l], nodes[2 * l + 1], ori, dir, t);
-        float d2 = aabb_test(nodes[2 * r], nodes[2 * r + 1], ori, dir, t);
+        uint32_t l = lf, rr = lf + 1;
+        float d1 = aabb_test<false>(nodes[2 * l], nodes[2 * l + 1], r, t);
+        float d2 = aabb_test<false>(nodes[2 * rr], nodes[2 * rr + 1], r, t);
         if (d1 > d2) {
             const float tt = d1; d1 = d2; d2 = tt;
-            const uint32_t x = l; l = r; r = x;
+            const uint32_t x = l; l = rr; rr = x;
         }
         if (d1 == kBig) {
             if (head == 0) break;
@@ -76,11 +178,20 @@ __device__ __forceinline__ bool intersect_bvh(const DevScene& sc, F3 ori, F3 dir
             node = l;
             if (d2 != kBig) {
                 if (head >= (uint32_t)kStackMax) return false;
-                stack[head++] = r;
+                stack[head++] = rr;
             }
         }
     }
     return true;
+}
+
+// Closest hit for one ray: production traversal with the exact fallback.
+template <bool kStats, typename Nodes, typename Stack>
+__device__ __forceinline__ bool closest_hit(const DevScene& sc, const Nodes& nodes, F3 o, F3 d, float& t,
+                                            uint32_t& index, Stack& stack, Counters& c) {
+    const Ray r = make_ray(o, d);
+    if (sc.fast_ok && ray_fast_ok(r)) return traverse<true, kStats>(sc, nodes, r, t, index, stack, c);
+    return traverse<false, kStats>(sc, nodes, r, t, index, stack, c);
 }
 
 // Path state carried across bounces.
@@ -130,9 +241,11 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
 }
 
 // Whole path (shaders.metal:302-344): returns sqrt(max(L, 0)).
-template <bool kStats, typename Stack>
-__device__ __forceinline__ F3 trace_path(const DevScene& sc, F3 ori, F3 dir, uint32_t seed, int bounce_limit,
-                                         int mirror_limit, Stack& stack, Counters& c, bool& overflow) {
+// kRef selects traverse_reference (MM_PIPE_REFERENCE).
+template <bool kStats, bool kRef, typename Nodes, typename Stack>
+__device__ __forceinline__ F3 trace_path(const DevScene& sc, const Nodes& nodes, F3 ori, F3 dir, uint32_t seed,
+                                         int bounce_limit, int mirror_limit, Stack& stack, Counters& c,
+                                         bool& overflow) {
     PathState p;
     p.ori = ori; p.dir = dir; p.seed = seed;
     p.T = F3{1.0f, 1.0f, 1.0f};
@@ -141,7 +254,9 @@ __device__ __forceinline__ F3 trace_path(const DevScene& sc, F3 ori, F3 dir, uin
     for (p.n = 0; p.n < bounce_limit + p.mh; ++p.n) {
         float t = kBig;
         uint32_t k = 0;
-        const bool ok = intersect_bvh<kStats>(sc, p.ori, p.dir, t, k, stack, c);
+        bool ok;
+        if constexpr (kRef) ok = traverse_reference<kStats>(sc, make_ray(p.ori, p.dir), t, k, stack, c);
+        else ok = closest_hit<kStats>(sc, nodes, p.ori, p.dir, t, k, stack, c);
         if (kStats) c.rays++;
         if (!ok) { overflow = true; break; }
         if (!shade_step(sc, p, t, k, mirror_limit)) break;

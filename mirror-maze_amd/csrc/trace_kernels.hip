@@ -24,8 +24,8 @@ __global__ void k_prep_rects(const mm_rect* __restrict__ rects, uint32_t n, floa
     const float lu = sqrtf(dot3(u, u));           // length(mirror.u), :61
     geo[4 * k + 0] = make_float4(o.x, o.y, o.z, lv);
     geo[4 * k + 1] = make_float4(nn.x, nn.y, nn.z, lu);
-    geo[4 * k + 2] = make_float4(v.x, v.y, v.z, 0.0f);
-    geo[4 * k + 3] = make_float4(u.x, u.y, u.z, 0.0f);
+    geo[4 * k + 2] = make_float4(v.x, v.y, v.z, 1.0f / lv);
+    geo[4 * k + 3] = make_float4(u.x, u.y, u.z, 1.0f / lu);
 }
 
 hipError_t launch_prep_rects(const mm_rect* rects_dev, uint32_t n, float4* geo_dev, hipStream_t s) {
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(1024) void k_trace_chunks(DevScene sc, mm_uniform u
     uint32_t stack[kStackMax];
     Counters c;
     bool overflow = false;
-    F3 s = trace_path<kStats>(sc, ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
+    F3 s = trace_path<kStats, false>(sc, sc.nodes, ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
     if (overflow) atomicOr(err, 1u);
     // level 1..3: test[f] += test[f+1], += test[f+2], += test[f+4]
     s = s + F3{__shfl_xor(s.x, 1), __shfl_xor(s.y, 1), __shfl_xor(s.z, 1)};
@@ -110,9 +110,16 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
 
 // ---------------------------------------------------------------------------
 // Throughput mode megakernel: path = pixel*spp + sample.
-template <bool kStats>
-__global__ __launch_bounds__(256) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
-                                                    unsigned long long* stats, uint32_t* err) {
+//   kRef  : traverse_reference (IEEE division everywhere), for A/B
+//   kLds  : stage the node array in LDS (dynamic shared memory) first
+template <bool kStats, bool kRef, bool kLds>
+__global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                     unsigned long long* stats, uint32_t* err) {
+    extern __shared__ float4 lds_nodes[];
+    if constexpr (kLds) {
+        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
+        __syncthreads();
+    }
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;
     const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
@@ -126,22 +133,39 @@ __global__ __launch_bounds__(256) void k_trace_mega(DevScene sc, TileJob job, fl
         const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
         uint32_t stack[kStackMax];
         bool overflow = false;
-        const F3 s = trace_path<kStats>(sc, ori, d, seed, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack,
-                                        c, overflow);
+        F3 s;
+        if constexpr (kLds)
+            s = trace_path<kStats, kRef>(sc, lds_nodes, ori, d, seed, (int)job.e.bounce_limit,
+                                         (int)job.e.mirror_limit, stack, c, overflow);
+        else
+            s = trace_path<kStats, kRef>(sc, sc.nodes, ori, d, seed, (int)job.e.bounce_limit,
+                                         (int)job.e.mirror_limit, stack, c, overflow);
         if (overflow) atomicOr(err, 1u);
         samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
     }
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
 }
 
-hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats_dev,
-                             uint32_t* err, bool count_stats, hipStream_t s) {
+template <bool kRef, bool kLds>
+static void launch_mega_t(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
+                          uint32_t* err, bool count_stats, uint32_t block, hipStream_t s) {
     const uint32_t n = job.w * job.h * job.e.spp;
-    const dim3 grid((n + 255) / 256);
+    const dim3 grid((n + block - 1) / block);
+    const size_t lds = kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0;
     if (count_stats)
-        hipLaunchKernelGGL(k_trace_mega<true>, grid, dim3(256), 0, s, sc, job, samples, stats_dev, err);
+        hipLaunchKernelGGL((k_trace_mega<true, kRef, kLds>), grid, dim3(block), lds, s, sc, job, samples, stats, err);
     else
-        hipLaunchKernelGGL(k_trace_mega<false>, grid, dim3(256), 0, s, sc, job, samples, stats_dev, err);
+        hipLaunchKernelGGL((k_trace_mega<false, kRef, kLds>), grid, dim3(block), lds, s, sc, job, samples, stats, err);
+}
+
+hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats_dev,
+                             uint32_t* err, bool count_stats, const MegaOpts& o, hipStream_t s) {
+    if (o.reference)
+        launch_mega_t<true, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
+    else if (o.lds_nodes)
+        launch_mega_t<false, true>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
+    else
+        launch_mega_t<false, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
     return hipGetLastError();
 }
 

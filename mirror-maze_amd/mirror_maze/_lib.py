@@ -32,7 +32,8 @@ class MMError(RuntimeError):
 MM_OK, MM_ERR_INVALID, MM_ERR_HIP, MM_ERR_NOMEM = 0, -1, -2, -3
 MM_ERR_NO_SCENE, MM_ERR_STACK, MM_ERR_UNSUPPORTED = -4, -5, -6
 MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE = 0x1, 0x2
-MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT = 0, 1, 2
+MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2, 3
+MM_OPT_LDS_NODES, MM_OPT_BLOCK = 1, 2
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
 
 
@@ -91,6 +92,7 @@ EXPORTS = {
     "mm_trace_tile": (C.c_int, [P, C.POINTER(mm_uniform), C.POINTER(mm_ext), C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_uint32, C.c_uint32, P, C.POINTER(mm_stats)]),
     "mm_set_pipeline": (C.c_int, [P, C.c_int]),
+    "mm_set_option": (C.c_int, [P, C.c_int, C.c_int]),
     "mm_sync": (C.c_int, [P]),
     "mm_last_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
     "mm_set_profiling": (C.c_int, [P, C.c_int]),

@@ -61,6 +61,9 @@ class Renderer:
     def set_pipeline(self, pipe: int) -> None:
         self._check(lib().mm_set_pipeline(self._ctx, pipe))
 
+    def set_option(self, key: int, value: int) -> None:
+        self._check(lib().mm_set_option(self._ctx, key, value))
+
     # -- scene ------------------------------------------------------------
     def upload_scene(self, s: Scene) -> None:
         rects = np.ascontiguousarray(s.rects, dtype=np.float32)

@@ -1,0 +1,80 @@
+"""A/B timing of the throughput-mode variants on one GPU (C3 unless told
+otherwise).  Every variant must produce the bit-identical frame; prints one
+line per variant with the HIP-event time of the trace kernel.
+
+    python scripts/ab_bench.py [--config c3] [--frames 3] [variant ...]
+variants: ref  mega-global  mega-lds  mega-lds-b512 ... (see VARIANTS)
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "mirror-maze_amd"))
+sys.path.insert(0, str(REPO))
+
+VARIANTS = {
+    "ref": dict(pipe=3),
+    "mega-global": dict(pipe=1, lds=0, block=256),
+    "mega-lds": dict(pipe=1, lds=1, block=256),
+    "mega-lds-b128": dict(pipe=1, lds=1, block=128),
+    "mega-lds-b512": dict(pipe=1, lds=1, block=512),
+    "mega-lds-b1024": dict(pipe=1, lds=1, block=1024),
+    "mega-global-b64": dict(pipe=1, lds=0, block=64),
+    "wave": dict(pipe=2),
+}
+
+
+def main():
+    import torch
+
+    from bench import CONFIGS
+    from mirror_maze import Renderer, Scene, default_uniform, make_ext
+    from mirror_maze._lib import MM_OPT_BLOCK, MM_OPT_LDS_NODES
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("variants", nargs="*", default=["ref", "mega-global", "mega-lds"])
+    a = ap.parse_args()
+    maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
+    scene = Scene.build(maze_n, 0)
+    u = default_uniform(W, H, 0)
+    base = None
+    print(f"# {desc}: {scene.n_rects} rects, {scene.n_nodes} nodes, depth {scene.bvh_depth}", flush=True)
+    for name in a.variants:
+        v = VARIANTS[name]
+        r = Renderer(0)
+        r.upload_scene(scene)
+        r.set_pipeline(v["pipe"])
+        if "lds" in v:
+            r.set_option(MM_OPT_LDS_NODES, v["lds"])
+        if "block" in v:
+            r.set_option(MM_OPT_BLOCK, v["block"])
+        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        _, st = r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, H, out=out, stats=True)  # warm
+        torch.cuda.synchronize()
+        r.set_profiling(True)
+        r.kernel_timing(reset=True)
+        t0 = time.perf_counter()
+        for f in range(a.frames):
+            r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, H, out=out)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / a.frames * 1e3
+        kms, kn = r.kernel_timing(reset=True)
+        k = kms / max(kn, 1)
+        same = "base"
+        if base is None:
+            base = out.clone()
+        else:
+            same = "bit-identical" if torch.equal(base.view(torch.int32), out.view(torch.int32)) else "MISMATCH"
+        print(f"{name:18s} trace {k:8.3f} ms  wall {wall:8.3f} ms/frame  {st.rays / k / 1e3:9.1f} Mrays/s  "
+              f"rays/frame {st.rays}  {same}", flush=True)
+        r.close()
+
+
+if __name__ == "__main__":
+    main()

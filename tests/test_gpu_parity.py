@@ -97,17 +97,31 @@ def test_c1_full_frame_matches_fixture_and_oracle(ren, gpu):
 WINDOWS = [(0, 0), (960, 540), (1888, 1064), (300, 700), (1500, 100)]
 
 
+PIPES = {  # (pipeline, {option: value})
+    "reference": (3, {}),
+    "mega-global": (1, {1: 0}),
+    "mega-lds": (1, {1: 1}),
+    "mega-lds-b1024": (1, {1: 1, 2: 1024}),
+}
+
+
+@pytest.mark.parametrize("pipe", sorted(PIPES))
 @pytest.mark.parametrize("cfg", [
     dict(n=16, spp=1, b=4, m=15),   # C2 settings
     dict(n=32, spp=8, b=8, m=8),    # C3 settings (the benchmark)
     dict(n=10, spp=3, b=5, m=15),   # non-multiple-of-8 spp
     dict(n=32, spp=16, b=8, m=15),  # C4 settings
 ])
-def test_tile_windows_bit_exact(ren, cfg):
-    from mirror_maze import default_uniform, make_ext
+def test_tile_windows_bit_exact(gpu, cfg, pipe):
+    from mirror_maze import Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 
     s = _scene(cfg["n"])
+    ren = Renderer(0)
+    p, opts = PIPES[pipe]
+    ren.set_pipeline(p)
+    for k, v in opts.items():
+        ren.set_option(k, v)
     ren.upload_scene(s)
     o = Oracle.from_scene(s)
     u = default_uniform(1920, 1080, 0)
@@ -119,6 +133,7 @@ def test_tile_windows_bit_exact(ren, cfg):
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
         assert (st.rays, st.node_visits, st.rect_tests, st.paths) == \
                (rst.rays, rst.node_visits, rst.rect_tests, rst.paths)
+    ren.close()
 
 
 def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
