@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "mm_device.h"
 
 namespace mm {
@@ -33,6 +35,19 @@ struct MegaOpts {
 hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples,
                              unsigned long long* stats_dev, uint32_t* err, bool count_stats,
                              const MegaOpts& o, hipStream_t s);
+
+struct PersistOpts {
+    bool lds_nodes = true;
+    uint32_t block = 512;
+    uint32_t threshold = 32;   // keep stepping traversals while > threshold lanes traverse
+    uint32_t grid_mult = 1;    // blocks = occupancy * CUs * grid_mult
+};
+
+// Throughput mode, persistent megakernel (trace_persist.hip).  `work` is a
+// device u32 path counter (zeroed by the launcher).
+hipError_t launch_trace_persist(const DevScene& sc, const TileJob& job, float4* samples,
+                                unsigned long long* stats_dev, uint32_t* err, uint32_t* work, bool count_stats,
+                                const PersistOpts& o, hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);

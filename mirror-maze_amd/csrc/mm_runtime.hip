@@ -54,6 +54,8 @@ struct mm_ctx {
     int pipe = MM_PIPE_AUTO;
     bool opt_lds = true;
     uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
+    bool opt_persist = false;  // measured slower on C3 (profiles/r01_ab_persist.txt)
+    uint32_t opt_threshold = 32;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
@@ -242,6 +244,11 @@ int mm_set_option(mm_ctx* c, int key, int value) {
     if (!c) return MM_ERR_INVALID;
     switch (key) {
         case MM_OPT_LDS_NODES: c->opt_lds = value != 0; return MM_OK;
+        case MM_OPT_PERSIST: c->opt_persist = value != 0; return MM_OK;
+        case MM_OPT_THRESHOLD:
+            if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "threshold must be 0..63");
+            c->opt_threshold = (uint32_t)value;
+            return MM_OK;
         case MM_OPT_BLOCK:
             if (value < 64 || value > 1024 || value % 64) return fail(c, MM_ERR_INVALID, "block must be 64..1024, x64");
             c->opt_block = (uint32_t)value;
@@ -389,12 +396,23 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         job.y_stride = y_stride;
         job.view_w = W;
         if ((rc = prof_mark(c))) return rc;
-        MegaOpts mo;
-        mo.reference = c->pipe == MM_PIPE_REFERENCE;
-        mo.lds_nodes = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
-        mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
-        HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux,
-                                  reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
+        const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
+        if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist) {
+            PersistOpts po;
+            po.lds_nodes = lds_fits;
+            po.block = c->opt_block ? c->opt_block : 512u;
+            po.threshold = c->opt_threshold;
+            HIPC(c, launch_trace_persist(dev_scene(c), job, c->d_samples, c->d_aux,
+                                         reinterpret_cast<uint32_t*>(c->d_aux + 4),
+                                         reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, po, c->stream));
+        } else {
+            MegaOpts mo;
+            mo.reference = c->pipe == MM_PIPE_REFERENCE;
+            mo.lds_nodes = lds_fits;
+            mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
+            HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux,
+                                      reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
+        }
         if ((rc = prof_mark(c))) return rc;
         HIPC(c, launch_resolve(job, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
         launches += 2;

@@ -107,43 +107,56 @@ __device__ __forceinline__ float aabb_test(float4 a, float4 b, const Ray& r, flo
 // upload from the reference's 32-B BVHNode):
 //     a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(packed), 0)
 // packed = count << 24 | left_first.  Children are adjacent, so an interior
-// visit loads one 64-B pair and already holds each child's (lf, count): only
-// a pop needs no load at all because the stack holds packed words.  Visit
-// order, pruning and pushes are exactly the reference's.
+// visit loads one 64-B pair and already holds each child's (lf, count); the
+// stack holds packed words, so a pop needs no node load.  Visit order,
+// pruning and pushes are exactly the reference's.
+//
+// trav_step runs ONE iteration of the reference's while(true) loop
+// (shaders.metal:126-155) on explicit state (cur, head, stack) and returns
+// true when the traversal is over (ovf set on stack overflow), so a caller
+// can interleave traversal steps of different rays (k_trace_persist).
+template <bool kFast, bool kStats, typename Nodes, typename Stack>
+__device__ __forceinline__ bool trav_step(const DevScene& sc, const Nodes& nodes, const Ray& r, float& t,
+                                          uint32_t& index, uint32_t& cur, uint32_t& head, Stack& stack,
+                                          Counters& c, bool& ovf) {
+    const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+    if (cnt > 0) {
+        for (uint32_t i = 0; i < cnt; ++i) rect_test<kFast>(sc.geo, sc.idx[lf + i], r, t, index);
+        if (kStats) c.rtests += cnt;
+        if (head == 0) return true;
+        cur = stack[--head];
+        return false;
+    }
+    if (kStats) c.visits++;
+    const float4 la = nodes[2 * lf], lb = nodes[2 * lf + 1], ra = nodes[2 * lf + 2], rb = nodes[2 * lf + 3];
+    float d1 = aabb_test<kFast>(la, lb, r, t);
+    float d2 = aabb_test<kFast>(ra, rb, r, t);
+    uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+    if (d1 > d2) {
+        const float tt = d1; d1 = d2; d2 = tt;
+        const uint32_t x = pl; pl = pr; pr = x;
+    }
+    if (d1 == kBig) {
+        if (head == 0) return true;
+        cur = stack[--head];
+    } else {
+        cur = pl;
+        if (d2 != kBig) {
+            if (head >= (uint32_t)kStackMax) { ovf = true; return true; }
+            stack[head++] = pr;
+        }
+    }
+    return false;
+}
+
 template <bool kFast, bool kStats, typename Nodes, typename Stack>
 __device__ __forceinline__ bool traverse(const DevScene& sc, const Nodes& nodes, const Ray& r, float& t,
                                          uint32_t& index, Stack& stack, Counters& c) {
     uint32_t cur = sc.root_packed, head = 0;
-    for (;;) {
-        const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
-        if (cnt > 0) {
-            for (uint32_t i = 0; i < cnt; ++i) rect_test<kFast>(sc.geo, sc.idx[lf + i], r, t, index);
-            if (kStats) c.rtests += cnt;
-            if (head == 0) break;
-            cur = stack[--head];
-            continue;
-        }
-        if (kStats) c.visits++;
-        const float4 la = nodes[2 * lf], lb = nodes[2 * lf + 1], ra = nodes[2 * lf + 2], rb = nodes[2 * lf + 3];
-        float d1 = aabb_test<kFast>(la, lb, r, t);
-        float d2 = aabb_test<kFast>(ra, rb, r, t);
-        uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
-        if (d1 > d2) {
-            const float tt = d1; d1 = d2; d2 = tt;
-            const uint32_t x = pl; pl = pr; pr = x;
-        }
-        if (d1 == kBig) {
-            if (head == 0) break;
-            cur = stack[--head];
-        } else {
-            cur = pl;
-            if (d2 != kBig) {
-                if (head >= (uint32_t)kStackMax) return false;
-                stack[head++] = pr;
-            }
-        }
+    bool ovf = false;
+    while (!trav_step<kFast, kStats>(sc, nodes, r, t, index, cur, head, stack, c, ovf)) {
     }
-    return true;
+    return !ovf;
 }
 
 // The straight statement of intersect_bvh_iterative over the reference node

@@ -18,14 +18,18 @@ sys.path.insert(0, str(REPO))
 
 VARIANTS = {
     "ref": dict(pipe=3),
-    "mega-global": dict(pipe=1, lds=0, block=256),
-    "mega-lds": dict(pipe=1, lds=1, block=256),
-    "mega-lds-b128": dict(pipe=1, lds=1, block=128),
-    "mega-lds-b512": dict(pipe=1, lds=1, block=512),
-    "mega-lds-b1024": dict(pipe=1, lds=1, block=1024),
-    "mega-global-b64": dict(pipe=1, lds=0, block=64),
+    "mega-global": dict(pipe=1, persist=0, lds=0, block=256),
+    "mega-lds": dict(pipe=1, persist=0, lds=1, block=256),
+    "mega-lds-b128": dict(pipe=1, persist=0, lds=1, block=128),
+    "mega-lds-b512": dict(pipe=1, persist=0, lds=1, block=512),
+    "mega-lds-b1024": dict(pipe=1, persist=0, lds=1, block=1024),
+    "mega-global-b64": dict(pipe=1, persist=0, lds=0, block=64),
     "wave": dict(pipe=2),
 }
+for _b in (256, 512):
+    for _th in (8, 16, 24, 32, 40, 48):
+        VARIANTS[f"persist-lds-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, th=_th)
+        VARIANTS[f"persist-global-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=0, block=_b, th=_th)
 
 
 def main():
@@ -33,7 +37,7 @@ def main():
 
     from bench import CONFIGS
     from mirror_maze import Renderer, Scene, default_uniform, make_ext
-    from mirror_maze._lib import MM_OPT_BLOCK, MM_OPT_LDS_NODES
+    from mirror_maze._lib import MM_OPT_BLOCK, MM_OPT_LDS_NODES, MM_OPT_PERSIST, MM_OPT_THRESHOLD
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
@@ -54,6 +58,10 @@ def main():
             r.set_option(MM_OPT_LDS_NODES, v["lds"])
         if "block" in v:
             r.set_option(MM_OPT_BLOCK, v["block"])
+        if "persist" in v:
+            r.set_option(MM_OPT_PERSIST, v["persist"])
+        if "th" in v:
+            r.set_option(MM_OPT_THRESHOLD, v["th"])
         out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
         _, st = r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, H, out=out, stats=True)  # warm
         torch.cuda.synchronize()

@@ -97,11 +97,14 @@ def test_c1_full_frame_matches_fixture_and_oracle(ren, gpu):
 WINDOWS = [(0, 0), (960, 540), (1888, 1064), (300, 700), (1500, 100)]
 
 
-PIPES = {  # (pipeline, {option: value})
+PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 threshold
     "reference": (3, {}),
-    "mega-global": (1, {1: 0}),
-    "mega-lds": (1, {1: 1}),
-    "mega-lds-b1024": (1, {1: 1, 2: 1024}),
+    "mega-global": (1, {1: 0, 3: 0}),
+    "mega-lds": (1, {1: 1, 3: 0}),
+    "mega-lds-b1024": (1, {1: 1, 2: 1024, 3: 0}),
+    "persist-lds": (1, {1: 1, 3: 1}),
+    "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
+    "persist-lds-t63-b256": (1, {1: 1, 3: 1, 4: 63, 2: 256}),
 }
 
 
