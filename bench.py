@@ -119,26 +119,21 @@ def main():
     ren = Renderer(local)
     ren.set_pipeline({"auto": MM_PIPE_AUTO, "mega": MM_PIPE_MEGAKERNEL, "wave": MM_PIPE_WAVEFRONT}[args.pipeline])
     ren.upload_scene(scene)
-    stream = torch.cuda.current_stream(dev)
-    ren.set_stream(stream)
     u = default_uniform(W, H, 0)
 
-    # rows r, r+world, ... ; pad so every rank sends the same shape
-    rows_max = (H + world - 1) // world
-    my_rows = len(range(rank, H, world))
-    tile = torch.zeros((rows_max, W, 4), dtype=torch.float32, device=dev)
-    gathered = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # rows r, r+world, ... (mirror_maze/dist.py); pad so every rank sends the same shape
+    from mirror_maze.dist import gather_frame, row_shard, rows_max
+
+    y0, y_stride, my_rows = row_shard(H, world, rank)
+    tile = torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev)
     frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
 
     def step(frame, stats=False):
         ext = make_ext(spp, bl, ml, frame=frame)
-        _, st = ren.trace_tile(u, ext, 0, rank, W, my_rows, y_stride=world, out=tile[:my_rows], stats=stats)
+        _, st = ren.trace_tile(u, ext, 0, y0, W, my_rows, y_stride=y_stride, out=tile[:my_rows], stats=stats)
         if world > 1:
-            dist.gather(tile, gathered, dst=0)
-            if rank == 0:  # de-interleave: row i*world + r <- gathered[r][i]
-                full = torch.stack(gathered, dim=1).reshape(rows_max * world, W, 4)
-                frame_buf.copy_(full[:H])
-        elif rank == 0:
+            gather_frame(tile, H, dst=0, out=frame_buf)  # one RCCL gather per frame
+        else:
             frame_buf.copy_(tile[:H])
         return st
 

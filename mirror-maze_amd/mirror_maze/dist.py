@@ -1,0 +1,53 @@
+"""Multi-GPU framebuffer sharding.
+
+One process per GPU.  The frame's rows are interleaved over ranks (rank r
+renders rows r, r+N, r+2N, ...), which balances the very uneven per-row cost
+(corridor rows vs wall rows) without any scheduling; the RNG is keyed on
+(pixel, sample, frame) so the N-GPU image equals the 1-GPU image bit for bit.
+At frame end one collective moves every tile to rank 0: torch.distributed's
+gather (RCCL send/recv over xGMI with the "nccl" backend; gloo on CPU for
+tests), then a de-interleave on rank 0.
+"""
+from __future__ import annotations
+
+
+def row_shard(height: int, world: int, rank: int):
+    """(y0, y_stride, rows) of this rank's interleaved row set."""
+    if not (0 <= rank < world):
+        raise ValueError("rank out of range")
+    return rank, world, len(range(rank, height, world))
+
+
+def rows_max(height: int, world: int) -> int:
+    """Rows every rank sends (the gather needs equal shapes; short ranks pad)."""
+    return (height + world - 1) // world
+
+
+def assemble(gathered, height: int):
+    """[world] x (rows_max, W, C) interleaved tiles -> (height, W, C) frame.
+    Row i*world + r of the frame is row i of rank r's tile."""
+    import torch
+
+    world = len(gathered)
+    rm, w, ch = gathered[0].shape
+    full = torch.stack(gathered, dim=1).reshape(rm * world, w, ch)
+    return full[:height]
+
+
+def gather_frame(tile, height: int, dst: int = 0, group=None, out=None):
+    """Gather every rank's (rows_max, W, C) tile to `dst` and return the
+    assembled frame there (None elsewhere).  `out` may receive the frame."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    gathered = [torch.empty_like(tile) for _ in range(world)] if rank == dst else None
+    dist.gather(tile, gathered, dst=dst, group=group)
+    if rank != dst:
+        return None
+    frame = assemble(gathered, height)
+    if out is not None:
+        out.copy_(frame)
+        return out
+    return frame
