@@ -99,8 +99,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 /* Tuning knobs (results never change; only speed does). */
 #define MM_OPT_LDS_NODES   1   /* 1: stage the BVH in LDS when it fits (default), 0: read via L1/L2 */
 #define MM_OPT_BLOCK       2   /* threads per workgroup for the megakernel (64..1024, multiple of 64) */
-#define MM_OPT_PERSIST     3   /* 1: persistent lane-refill megakernel, 0: one thread per path (default) */
+#define MM_OPT_PERSIST     3   /* 0: one thread per path, 1: persistent lane-refill megakernel,
+                                  2: wave-persistent megakernel, 64-path chunks (default) */
 #define MM_OPT_THRESHOLD   4   /* persistent kernel: traverse while > N lanes traverse (0..63) */
+#define MM_OPT_MIN_WAVES   5   /* wave-persistent kernel register budget: 1, 6 or 8 (default) waves/SIMD */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Wait for all work queued by this context. */

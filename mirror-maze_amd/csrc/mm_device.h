@@ -19,7 +19,9 @@ constexpr int kStackMax = 50;     // shaders.metal:123
 // ---- HBM layouts ------------------------------------------------------------
 // Reference node (nodes_ref): 2 x float4 = the reference's 32-B bvh_node,
 //   a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(left_first), bits(count))
-// Production node (nodes): same a; b = (mx.y, mx.z, bits(count<<24 | left_first), 0).
+// Production node (nodes): a = (mn.x, mx.x, mn.y, mx.y),
+//   b = (mn.z, mx.z, bits(count<<24 | left_first), 0): bounds as per-axis
+//   (min, max) pairs for packed math.
 // Children of an interior node are adjacent (left_first, left_first+1), so the
 // pair a traversal step reads is one contiguous 64-B line.
 //

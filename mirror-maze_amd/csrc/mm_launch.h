@@ -36,6 +36,12 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
                              unsigned long long* stats_dev, uint32_t* err, bool count_stats,
                              const MegaOpts& o, hipStream_t s);
 
+// Throughput mode, wave-persistent megakernel: resident blocks, waves pull
+// 64-path chunks from `work` (zeroed by the launcher).
+hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
+                                    unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
+                                    bool lds_nodes, uint32_t block, uint32_t min_waves, hipStream_t s);
+
 struct PersistOpts {
     bool lds_nodes = true;
     uint32_t block = 512;
@@ -48,6 +54,35 @@ struct PersistOpts {
 hipError_t launch_trace_persist(const DevScene& sc, const TileJob& job, float4* samples,
                                 unsigned long long* stats_dev, uint32_t* err, uint32_t* work, bool count_stats,
                                 const PersistOpts& o, hipStream_t s);
+
+// ---- wavefront pipeline (trace_wave.hip) ---------------------------------------
+struct WaveState {
+    // SoA path state, indexed by path id (capacity entries each)
+    float* ox; float* oy; float* oz;
+    float* dx; float* dy; float* dz;
+    float* tr; float* tg; float* tb;    // throughput T
+    float* lr; float* lg; float* lb;    // radiance L
+    uint32_t* seed;
+    uint32_t* nm;                       // n | mirror_hits << 16
+    float* hit_t;
+    uint32_t* hit_i;
+    uint32_t* queue[2];                 // live path ids (ping / pong)
+    uint32_t* counters;                 // [0], [1]: queue lengths
+    uint32_t capacity;
+};
+
+struct WaveOpts {
+    bool lds_nodes = true;
+    uint32_t block = 512;               // extend kernel
+    uint32_t extend_blocks = 2048;      // grid cap (grid-stride over the queue)
+};
+
+hipError_t launch_wf_generate(const TileJob& job, const WaveState& ws, float4* samples, hipStream_t s);
+hipError_t launch_wf_extend(const DevScene& sc, const WaveState& ws, int q, uint32_t n_upper,
+                            unsigned long long* stats, bool count_stats, const WaveOpts& o, hipStream_t s);
+hipError_t launch_wf_shade(const DevScene& sc, const TileJob& job, const WaveState& ws, int q, uint32_t n_upper,
+                           float4* samples, unsigned long long* stats, uint32_t* err, bool count_stats,
+                           hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);

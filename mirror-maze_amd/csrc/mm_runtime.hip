@@ -46,6 +46,9 @@ struct mm_ctx {
     // per-sample staging (throughput mode)
     float4* d_samples = nullptr;
     size_t samples_cap = 0;
+    // wavefront SoA state (MM_PIPE_WAVEFRONT)
+    void* d_wave = nullptr;
+    size_t wave_cap = 0;      // paths
     // aux: stats[4] (u64) + error flag (u32)
     unsigned long long* d_aux = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -54,7 +57,10 @@ struct mm_ctx {
     int pipe = MM_PIPE_AUTO;
     bool opt_lds = true;
     uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
-    bool opt_persist = false;  // measured slower on C3 (profiles/r01_ab_persist.txt)
+    // Megakernel form (measured on C3, profiles/r01_ab_*.txt): wave-persistent
+    // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
+    int opt_persist = 2;         // 0 one thread per path, 1 lane refill, 2 wave-persistent
+    uint32_t opt_min_waves = 8;  // wave-persistent launch bound (waves per SIMD)
     uint32_t opt_threshold = 32;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
     bool prof = false;
@@ -144,6 +150,32 @@ bool extent_ok(float x) {
     return a == 0.0f || (a >= 0x1p-10f && a <= 0x1p60f);
 }
 
+// Carve the wavefront SoA buffers for `n` paths out of one allocation.
+int wave_state(mm_ctx* c, uint32_t n, WaveState& ws) {
+    const size_t n4 = ((size_t)n + 63) & ~(size_t)63;  // 256-B aligned arrays
+    const size_t words = 16 * n4 + 2 * n4 + 64;
+    if (c->wave_cap < n || !c->d_wave) {
+        (void)hipFree(c->d_wave);
+        c->d_wave = nullptr;
+        c->wave_cap = 0;
+        HIPC(c, hipMalloc(&c->d_wave, words * 4));
+        c->wave_cap = n;
+    }
+    const size_t cap4 = (((size_t)c->wave_cap) + 63) & ~(size_t)63;
+    float* f = reinterpret_cast<float*>(c->d_wave);
+    uint32_t* u = reinterpret_cast<uint32_t*>(c->d_wave);
+    ws.ox = f + 0 * cap4; ws.oy = f + 1 * cap4; ws.oz = f + 2 * cap4;
+    ws.dx = f + 3 * cap4; ws.dy = f + 4 * cap4; ws.dz = f + 5 * cap4;
+    ws.tr = f + 6 * cap4; ws.tg = f + 7 * cap4; ws.tb = f + 8 * cap4;
+    ws.lr = f + 9 * cap4; ws.lg = f + 10 * cap4; ws.lb = f + 11 * cap4;
+    ws.seed = u + 12 * cap4; ws.nm = u + 13 * cap4;
+    ws.hit_t = f + 14 * cap4; ws.hit_i = u + 15 * cap4;
+    ws.queue[0] = u + 16 * cap4; ws.queue[1] = u + 17 * cap4;
+    ws.counters = u + 18 * cap4;
+    ws.capacity = c->wave_cap;
+    return MM_OK;
+}
+
 int begin_timing(mm_ctx* c) {
     HIPC(c, hipEventRecord(c->ev0, c->stream));
     return MM_OK;
@@ -217,7 +249,7 @@ void mm_destroy(mm_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_scene(c);
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
-    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux);
+    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -244,10 +276,17 @@ int mm_set_option(mm_ctx* c, int key, int value) {
     if (!c) return MM_ERR_INVALID;
     switch (key) {
         case MM_OPT_LDS_NODES: c->opt_lds = value != 0; return MM_OK;
-        case MM_OPT_PERSIST: c->opt_persist = value != 0; return MM_OK;
+        case MM_OPT_PERSIST:
+            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "persist must be 0, 1 or 2");
+            c->opt_persist = value;
+            return MM_OK;
         case MM_OPT_THRESHOLD:
             if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "threshold must be 0..63");
             c->opt_threshold = (uint32_t)value;
+            return MM_OK;
+        case MM_OPT_MIN_WAVES:
+            if (value != 1 && value != 6 && value != 8) return fail(c, MM_ERR_INVALID, "min waves must be 1, 6 or 8");
+            c->opt_min_waves = (uint32_t)value;
             return MM_OK;
         case MM_OPT_BLOCK:
             if (value < 64 || value > 1024 || value % 64) return fail(c, MM_ERR_INVALID, "block must be 64..1024, x64");
@@ -266,13 +305,18 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     std::string why;
     int rc = check_tree(nodes, n_nodes, idx, n_rects, why);
     if (rc != MM_OK) return fail(c, rc, "mm_upload_scene: " + why);
-    // production node layout: b.z = count << 24 | left_first
-    std::vector<mm_node> packed(nodes, nodes + n_nodes);
+    // production node layout: a = (mn.x, mx.x, mn.y, mx.y), b = (mn.z, mx.z, packed, 0),
+    // packed = count << 24 | left_first
+    std::vector<float4> packed(2 * (size_t)n_nodes);
     for (uint32_t i = 0; i < n_nodes; ++i) {
-        if (nodes[i].count >= 256u || nodes[i].left_first >= (1u << 24))
+        const mm_node& nd = nodes[i];
+        if (nd.count >= 256u || nd.left_first >= (1u << 24))
             return fail(c, MM_ERR_UNSUPPORTED, "mm_upload_scene: leaf with >= 256 planes or index >= 2^24");
-        packed[i].left_first = (nodes[i].count << 24) | nodes[i].left_first;
-        packed[i].count = 0;
+        uint32_t pk = (nd.count << 24) | nd.left_first;
+        float pkf;
+        std::memcpy(&pkf, &pk, 4);
+        packed[2 * i] = make_float4(nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1]);
+        packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
     }
     bool fast = true;
     for (uint32_t i = 0; i < n_nodes && fast; ++i)
@@ -296,14 +340,14 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     HIPC(c, hipMemcpyAsync(c->d_rects, rects, n_rects * sizeof(mm_rect), hipMemcpyHostToDevice, c->stream));
     // mm_node is exactly two float4: (mn.xyz, mx.x) (mx.yz, left_first, count)
     HIPC(c, hipMemcpyAsync(c->d_nodes_ref, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMemcpyAsync(c->d_nodes, packed.data(), n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_nodes, packed.data(), packed.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_idx, idx, n_rects * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));  // host arrays may be freed on return
     c->n_rects = n_rects;
     c->n_nodes = n_nodes;
-    c->root_packed = packed[0].left_first;
+    c->root_packed = (nodes[0].count << 24) | nodes[0].left_first;
     c->fast_ok = fast;
     c->has_scene = true;
     return MM_OK;
@@ -378,7 +422,9 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
     const bool want_stats = (e->flags & MM_EXT_COUNT_STATS) != 0;
     // Bound the per-sample staging buffer: process whole rows, <= 64 Mi paths.
     const uint64_t row_paths = (uint64_t)w * e->spp;
-    const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, (64ull << 20) / row_paths));
+    const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
+    const uint64_t batch_paths = wave ? (32ull << 20) : (64ull << 20);
+    const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
     int rc = ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
     if (rc) return rc;
@@ -397,7 +443,31 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         job.view_w = W;
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
-        if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist) {
+        if (wave) {
+            const uint32_t n = job.w * job.h * job.e.spp;
+            WaveState ws;
+            if ((rc = wave_state(c, n, ws))) return rc;
+            WaveOpts wo;
+            wo.lds_nodes = lds_fits;
+            if (c->opt_block) wo.block = c->opt_block;
+            uint32_t* err = reinterpret_cast<uint32_t*>(c->d_aux + 4);
+            HIPC(c, launch_wf_generate(job, ws, c->d_samples, c->stream));
+            const int max_rays = (int)job.e.bounce_limit + std::max(0, (int)job.e.mirror_limit - 1);
+            for (int it = 0; it < max_rays; ++it) {
+                if ((rc = prof_mark(c))) return rc;
+                HIPC(c, launch_wf_extend(dev_scene(c), ws, it & 1, n, c->d_aux, want_stats, wo, c->stream));
+                if ((rc = prof_mark(c))) return rc;
+                HIPC(c, launch_wf_shade(dev_scene(c), job, ws, it & 1, n, c->d_samples, c->d_aux, err, want_stats,
+                                        c->stream));
+                launches += 2;
+            }
+            launches += 1;
+        } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
+            HIPC(c, launch_trace_wavepersist(dev_scene(c), job, c->d_samples, c->d_aux,
+                                             reinterpret_cast<uint32_t*>(c->d_aux + 4),
+                                             reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, lds_fits,
+                                             c->opt_block ? c->opt_block : 1024u, c->opt_min_waves, c->stream));
+        } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
             PersistOpts po;
             po.lds_nodes = lds_fits;
             po.block = c->opt_block ? c->opt_block : 512u;

@@ -102,10 +102,28 @@ __device__ __forceinline__ float aabb_test(float4 a, float4 b, const Ray& r, flo
     return (tmax >= tmin && tmin < t && tmax > 0.0f) ? tmin : kBig;
 }
 
+// Slab test on the production node layout, bounds as (min, max) pairs per
+// axis: a = (mn.x, mx.x, mn.y, mx.y), b = (mn.z, mx.z, packed, 0).  Scalar
+// ops: gfx950's v_pk_fma_f32 runs at the same FLOP rate as v_fma_f32 and the
+// register pairs cost occupancy (measured 13.6 vs 12.85 ms/frame on C3,
+// profiles/r01_ab_packed.txt).  Same values as aabb_test.
+template <bool kFast>
+__device__ __forceinline__ float aabb_pairs(float4 a, float4 b, const Ray& r, float t) {
+    const float tx1 = sdiv<kFast>(a.x - r.o.x, r.d.x, r.y.x), tx2 = sdiv<kFast>(a.y - r.o.x, r.d.x, r.y.x);
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    const float ty1 = sdiv<kFast>(a.z - r.o.y, r.d.y, r.y.y), ty2 = sdiv<kFast>(a.w - r.o.y, r.d.y, r.y.y);
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    tmax = fminf(tmax, fmaxf(ty1, ty2));
+    const float tz1 = sdiv<kFast>(b.x - r.o.z, r.d.z, r.y.z), tz2 = sdiv<kFast>(b.y - r.o.z, r.d.z, r.y.z);
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    tmax = fminf(tmax, fmaxf(tz1, tz2));
+    return (tmax >= tmin && tmin < t && tmax > 0.0f) ? tmin : kBig;
+}
+
 // ---------------------------------------------------------------------------
 // intersect_bvh_iterative, production form.  Device node layout (built at
 // upload from the reference's 32-B BVHNode):
-//     a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(packed), 0)
+//     a = (mn.x, mx.x, mn.y, mx.y)   b = (mn.z, mx.z, bits(packed), 0)
 // packed = count << 24 | left_first.  Children are adjacent, so an interior
 // visit loads one 64-B pair and already holds each child's (lf, count); the
 // stack holds packed words, so a pop needs no node load.  Visit order,
@@ -129,8 +147,8 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const Nodes& nodes
     }
     if (kStats) c.visits++;
     const float4 la = nodes[2 * lf], lb = nodes[2 * lf + 1], ra = nodes[2 * lf + 2], rb = nodes[2 * lf + 3];
-    float d1 = aabb_test<kFast>(la, lb, r, t);
-    float d2 = aabb_test<kFast>(ra, rb, r, t);
+    float d1 = aabb_pairs<kFast>(la, lb, r, t);
+    float d2 = aabb_pairs<kFast>(ra, rb, r, t);
     uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
     if (d1 > d2) {
         const float tt = d1; d1 = d2; d2 = tt;

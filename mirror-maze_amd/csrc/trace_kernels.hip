@@ -146,6 +146,92 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
 }
 
+// Wave-persistent megakernel: resident blocks (LDS filled once per block);
+// each wave takes 64 consecutive paths at a time from a global counter and
+// traces them exactly like k_trace_mega, so no block waits for its slowest
+// wave before the CU can take more work.
+template <bool kStats, typename Nodes>
+__device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes& nodes, const TileJob& job,
+                                                 float4* __restrict__ samples, unsigned long long* stats,
+                                                 uint32_t* err, uint32_t* work) {
+    const uint32_t spp = job.e.spp;
+    const uint32_t n_paths = job.w * job.h * spp;
+    const uint32_t lane = threadIdx.x & 63u;
+    const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
+    Counters c;
+    uint32_t paths = 0;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(work, 64u);
+        base = __shfl(base, 0);
+        if (base >= n_paths) break;
+        const uint32_t path = base + lane;
+        if (path < n_paths) {
+            const uint32_t pix = path / spp, smp = path - pix * spp;
+            const uint32_t j = pix / job.w, i = pix - j * job.w;
+            const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
+            uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
+            const F3 d = jitter(primary_dir(job.u, px, py), seed);
+            uint32_t stack[kStackMax];
+            bool overflow = false;
+            const F3 s = trace_path<kStats, false>(sc, nodes, ori, d, seed, (int)job.e.bounce_limit,
+                                                   (int)job.e.mirror_limit, stack, c, overflow);
+            if (overflow) atomicOr(err, 1u);
+            samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
+            paths++;
+        }
+    }
+    if (kStats) flush_stats(stats, c, paths);
+}
+
+template <bool kStats, bool kLds, int kBlock, int kMinWaves>
+__global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                            unsigned long long* stats, uint32_t* err, uint32_t* work) {
+    if constexpr (kLds) {
+        extern __shared__ float4 lds_nodes[];
+        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
+        __syncthreads();
+        wavepersist_body<kStats>(sc, lds_nodes, job, samples, stats, err, work);
+    } else {
+        wavepersist_body<kStats>(sc, sc.nodes, job, samples, stats, err, work);
+    }
+}
+
+template <bool kLds, int kBlock, int kMinWaves>
+static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
+                                       unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
+                                       hipStream_t s) {
+    const uint32_t block = kBlock;
+    const size_t lds = kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0;
+    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves>
+                            : k_trace_wavepersist<false, kLds, kBlock, kMinWaves>;
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
+    if (e != hipSuccess) return e;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t n_paths = job.w * job.h * job.e.spp;
+    uint32_t grid = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus);
+    grid = std::max(1u, std::min(grid, (n_paths + block - 1) / block));
+    e = hipMemsetAsync(work, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, s, sc, job, samples, stats, err, work);
+    return hipGetLastError();
+}
+
+// Register budget by launch bounds: waves/SIMD = 8 -> <= 64 VGPRs.
+hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
+                                    unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
+                                    bool lds_nodes, uint32_t block, uint32_t min_waves, hipStream_t s) {
+#define MM_WP(B, W)                                                                                  \
+    if (block == B && min_waves == W)                                                                \
+        return lds_nodes ? launch_wavepersist_t<true, B, W>(sc, job, samples, stats, err, work, count_stats, s) \
+                         : launch_wavepersist_t<false, B, W>(sc, job, samples, stats, err, work, count_stats, s);
+    MM_WP(256, 1) MM_WP(256, 8) MM_WP(512, 1) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
+#undef MM_WP
+    return hipErrorInvalidValue;
+}
+
 template <bool kRef, bool kLds>
 static void launch_mega_t(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
                           uint32_t* err, bool count_stats, uint32_t block, hipStream_t s) {

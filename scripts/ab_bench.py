@@ -25,7 +25,12 @@ VARIANTS = {
     "mega-lds-b1024": dict(pipe=1, persist=0, lds=1, block=1024),
     "mega-global-b64": dict(pipe=1, persist=0, lds=0, block=64),
     "wave": dict(pipe=2),
+    "wave-global": dict(pipe=2, lds=0),
+    "wave-b256": dict(pipe=2, block=256),
 }
+for _b, _w in ((256, 1), (256, 8), (512, 1), (512, 6), (512, 8), (1024, 1), (1024, 8)):
+    VARIANTS[f"wp-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w)
+    VARIANTS[f"wp-global-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=0, block=_b, mw=_w)
 for _b in (256, 512):
     for _th in (8, 16, 24, 32, 40, 48):
         VARIANTS[f"persist-lds-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, th=_th)
@@ -37,7 +42,7 @@ def main():
 
     from bench import CONFIGS
     from mirror_maze import Renderer, Scene, default_uniform, make_ext
-    from mirror_maze._lib import MM_OPT_BLOCK, MM_OPT_LDS_NODES, MM_OPT_PERSIST, MM_OPT_THRESHOLD
+    from mirror_maze._lib import MM_OPT_BLOCK, MM_OPT_LDS_NODES, MM_OPT_MIN_WAVES, MM_OPT_PERSIST, MM_OPT_THRESHOLD
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
@@ -60,6 +65,8 @@ def main():
             r.set_option(MM_OPT_BLOCK, v["block"])
         if "persist" in v:
             r.set_option(MM_OPT_PERSIST, v["persist"])
+        if "mw" in v:
+            r.set_option(MM_OPT_MIN_WAVES, v["mw"])
         if "th" in v:
             r.set_option(MM_OPT_THRESHOLD, v["th"])
         out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")

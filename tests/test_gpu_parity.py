@@ -105,6 +105,11 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "persist-lds": (1, {1: 1, 3: 1}),
     "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
     "persist-lds-t63-b256": (1, {1: 1, 3: 1, 4: 63, 2: 256}),
+    "wavepersist-lds": (1, {1: 1, 3: 2}),
+    "wavepersist-lds-b512-w8": (1, {1: 1, 3: 2, 2: 512, 5: 8}),
+    "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
+    "wavefront": (2, {}),
+    "wavefront-global": (2, {1: 0}),
 }
 
 
