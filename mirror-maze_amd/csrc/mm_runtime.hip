@@ -31,6 +31,8 @@ struct mm_ctx {
     float4* d_nodes_ref = nullptr;  // reference layout
     uint32_t root_packed = 0;
     bool fast_ok = false;
+    uint32_t depth = 0;         // tree depth = max traversal stack entries
+    bool stack16_ok = false;    // every node packs into 16 bits (count < 16, left_first < 4096)
     float4* d_geo = nullptr;
     float4* d_shade = nullptr;
     uint32_t* d_idx = nullptr;
@@ -61,6 +63,7 @@ struct mm_ctx {
     // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
     int opt_persist = 2;         // 0 one thread per path, 1 lane refill, 2 wave-persistent
     uint32_t opt_min_waves = 8;  // wave-persistent launch bound (waves per SIMD)
+    int opt_lds_stack = 0;       // u16 LDS stack: measured equal to scratch (profiles/r01_ab_ldsstack.txt)
     uint32_t opt_threshold = 32;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
     bool prof = false;
@@ -114,7 +117,8 @@ void free_scene(mm_ctx* c) {
 
 // Stack depth the near-first traversal can reach: at most one pending far
 // child per level, so the tree depth bounds it.
-int check_tree(const mm_node* nodes, uint32_t n_nodes, const uint32_t* idx, uint32_t n_rects, std::string& why) {
+int check_tree(const mm_node* nodes, uint32_t n_nodes, const uint32_t* idx, uint32_t n_rects, std::string& why,
+               uint32_t* depth_out) {
     for (uint32_t i = 0; i < n_rects; ++i)
         if (idx[i] >= n_rects) { why = "idx out of range"; return MM_ERR_INVALID; }
     std::vector<std::pair<uint32_t, uint32_t>> todo{{0u, 0u}};
@@ -136,6 +140,7 @@ int check_tree(const mm_node* nodes, uint32_t n_nodes, const uint32_t* idx, uint
         }
     }
     if (maxd > (uint32_t)kStackMax) { why = "BVH deeper than the 50-entry traversal stack"; return MM_ERR_STACK; }
+    *depth_out = maxd;
     return MM_OK;
 }
 
@@ -284,6 +289,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "threshold must be 0..63");
             c->opt_threshold = (uint32_t)value;
             return MM_OK;
+        case MM_OPT_LDS_STACK: c->opt_lds_stack = value != 0; return MM_OK;
         case MM_OPT_MIN_WAVES:
             if (value != 1 && value != 6 && value != 8) return fail(c, MM_ERR_INVALID, "min waves must be 1, 6 or 8");
             c->opt_min_waves = (uint32_t)value;
@@ -303,7 +309,8 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         return fail(c, MM_ERR_INVALID, "mm_upload_scene: null array or empty scene");
     if (n_nodes > 2 * n_rects) return fail(c, MM_ERR_INVALID, "mm_upload_scene: more than 2n-1 nodes");
     std::string why;
-    int rc = check_tree(nodes, n_nodes, idx, n_rects, why);
+    uint32_t depth = 0;
+    int rc = check_tree(nodes, n_nodes, idx, n_rects, why, &depth);
     if (rc != MM_OK) return fail(c, rc, "mm_upload_scene: " + why);
     // production node layout: a = (mn.x, mx.x, mn.y, mx.y), b = (mn.z, mx.z, packed, 0),
     // packed = count << 24 | left_first
@@ -348,6 +355,10 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     c->n_rects = n_rects;
     c->n_nodes = n_nodes;
     c->root_packed = (nodes[0].count << 24) | nodes[0].left_first;
+    c->depth = depth;
+    c->stack16_ok = true;
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        if (nodes[i].count >= 16u || nodes[i].left_first >= 4096u) c->stack16_ok = false;
     c->fast_ok = fast;
     c->has_scene = true;
     return MM_OK;
@@ -463,10 +474,16 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             }
             launches += 1;
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
+            const uint32_t block = c->opt_block ? c->opt_block : 1024u;
+            const uint32_t slots = std::max(1u, c->depth);
+            // keep 2 blocks of 1024 (or their equivalent) resident: <= 80 KB of LDS per block
+            const size_t lds_total = 2 * (size_t)c->n_nodes * sizeof(float4) + (size_t)slots * block * 2;
+            const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= (size_t)(160 * 1024) * block / 2048;
+            const int mode = lds_fits ? (stack_fits ? 2 : 1) : 0;
             HIPC(c, launch_trace_wavepersist(dev_scene(c), job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
-                                             reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, lds_fits,
-                                             c->opt_block ? c->opt_block : 1024u, c->opt_min_waves, c->stream));
+                                             reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, mode, slots,
+                                             block, c->opt_min_waves, c->stream));
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
             PersistOpts po;
             po.lds_nodes = lds_fits;

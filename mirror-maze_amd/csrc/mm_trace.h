@@ -121,6 +121,34 @@ __device__ __forceinline__ float aabb_pairs(float4 a, float4 b, const Ray& r, fl
 }
 
 // ---------------------------------------------------------------------------
+// Traversal stack policies.  Entries are packed child words
+// (count << 24 | left_first).  The stack never holds more entries than the
+// tree is deep (one pending far child per level of the current path).
+struct ScratchStack {          // the reference's 50-entry private array
+    uint32_t s[kStackMax];
+    static constexpr uint32_t kCap = kStackMax;
+    __device__ __forceinline__ void push(uint32_t i, uint32_t v) { s[i] = v; }
+    __device__ __forceinline__ uint32_t pop(uint32_t i) const { return s[i]; }
+};
+// u16 entries in LDS, [slot][thread] so a wave's same-slot accesses are
+// contiguous: (count << 12 | left_first) needs count < 16, left_first < 4096
+// and slots >= tree depth -- all checked at upload.
+struct LdsStack16 {
+    uint16_t* base;            // &lds[slot 0][this thread]
+    uint32_t stride;           // threads per block
+    uint32_t cap;
+    __device__ __forceinline__ void push(uint32_t i, uint32_t v) {
+        base[i * stride] = (uint16_t)(((v >> 24) << 12) | (v & 0xFFFu));
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t i) const {
+        const uint32_t p = base[i * stride];
+        return ((p >> 12) << 24) | (p & 0xFFFu);
+    }
+};
+template <typename S> __device__ __forceinline__ uint32_t stack_cap(const S& st) { return st.kCap; }
+template <> __device__ __forceinline__ uint32_t stack_cap<LdsStack16>(const LdsStack16& st) { return st.cap; }
+
+// ---------------------------------------------------------------------------
 // intersect_bvh_iterative, production form.  Device node layout (built at
 // upload from the reference's 32-B BVHNode):
 //     a = (mn.x, mx.x, mn.y, mx.y)   b = (mn.z, mx.z, bits(packed), 0)
@@ -142,7 +170,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const Nodes& nodes
         for (uint32_t i = 0; i < cnt; ++i) rect_test<kFast>(sc.geo, sc.idx[lf + i], r, t, index);
         if (kStats) c.rtests += cnt;
         if (head == 0) return true;
-        cur = stack[--head];
+        cur = stack.pop(--head);
         return false;
     }
     if (kStats) c.visits++;
@@ -156,12 +184,12 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const Nodes& nodes
     }
     if (d1 == kBig) {
         if (head == 0) return true;
-        cur = stack[--head];
+        cur = stack.pop(--head);
     } else {
         cur = pl;
         if (d2 != kBig) {
-            if (head >= (uint32_t)kStackMax) { ovf = true; return true; }
-            stack[head++] = pr;
+            if (head >= stack_cap(stack)) { ovf = true; return true; }
+            stack.push(head++, pr);
         }
     }
     return false;
@@ -191,7 +219,7 @@ __device__ __forceinline__ bool traverse_reference(const DevScene& sc, const Ray
             for (uint32_t i = 0; i < count; ++i) rect_test<false>(sc.geo, sc.idx[lf + i], r, t, index);
             if (kStats) c.rtests += count;
             if (head == 0) break;
-            node = stack[--head];
+            node = stack.pop(--head);
             continue;
         }
         if (kStats) c.visits++;
@@ -204,12 +232,12 @@ __device__ __forceinline__ bool traverse_reference(const DevScene& sc, const Ray
         }
         if (d1 == kBig) {
             if (head == 0) break;
-            node = stack[--head];
+            node = stack.pop(--head);
         } else {
             node = l;
             if (d2 != kBig) {
                 if (head >= (uint32_t)kStackMax) return false;
-                stack[head++] = rr;
+                stack.push(head++, rr);
             }
         }
     }

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(1024) void k_trace_chunks(DevScene sc, mm_uniform u
     uint32_t seed = seed_reference(gx * 32 + lx, gy * 32 + ly, u.time);
     const F3 d = jitter(primary_dir(u, px, py), seed);
     const F3 ori = F3{u.cam.center[0], u.cam.center[1], u.cam.center[2]};
-    uint32_t stack[kStackMax];
+    ScratchStack stack;
     Counters c;
     bool overflow = false;
     F3 s = trace_path<kStats, false>(sc, sc.nodes, ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
         uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
         const F3 d = jitter(primary_dir(job.u, px, py), seed);
         const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
-        uint32_t stack[kStackMax];
+        ScratchStack stack;
         bool overflow = false;
         F3 s;
         if constexpr (kLds)
@@ -150,10 +150,10 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // each wave takes 64 consecutive paths at a time from a global counter and
 // traces them exactly like k_trace_mega, so no block waits for its slowest
 // wave before the CU can take more work.
-template <bool kStats, typename Nodes>
-__device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes& nodes, const TileJob& job,
-                                                 float4* __restrict__ samples, unsigned long long* stats,
-                                                 uint32_t* err, uint32_t* work) {
+template <bool kStats, typename Nodes, typename Stack>
+__device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes& nodes, Stack& stack,
+                                                 const TileJob& job, float4* __restrict__ samples,
+                                                 unsigned long long* stats, uint32_t* err, uint32_t* work) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;
     const uint32_t lane = threadIdx.x & 63u;
@@ -172,7 +172,6 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes
             const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
             uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
             const F3 d = jitter(primary_dir(job.u, px, py), seed);
-            uint32_t stack[kStackMax];
             bool overflow = false;
             const F3 s = trace_path<kStats, false>(sc, nodes, ori, d, seed, (int)job.e.bounce_limit,
                                                    (int)job.e.mirror_limit, stack, c, overflow);
@@ -184,25 +183,40 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes
     if (kStats) flush_stats(stats, c, paths);
 }
 
-template <bool kStats, bool kLds, int kBlock, int kMinWaves>
-__global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
-                                                            unsigned long long* stats, uint32_t* err, uint32_t* work) {
-    if constexpr (kLds) {
+// kLds: 0 nodes via L1/L2 + scratch stack, 1 nodes in LDS + scratch stack,
+// 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread).
+template <bool kStats, int kLds, int kBlock, int kMinWaves>
+__global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
+                                                                         float4* __restrict__ samples,
+                                                                         unsigned long long* stats, uint32_t* err,
+                                                                         uint32_t* work, uint32_t stack_slots) {
+    if constexpr (kLds > 0) {
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
         __syncthreads();
-        wavepersist_body<kStats>(sc, lds_nodes, job, samples, stats, err, work);
+        if constexpr (kLds == 2) {
+            LdsStack16 st;
+            st.base = reinterpret_cast<uint16_t*>(lds_nodes + 2 * sc.n_nodes) + threadIdx.x;
+            st.stride = blockDim.x;
+            st.cap = stack_slots;
+            wavepersist_body<kStats>(sc, lds_nodes, st, job, samples, stats, err, work);
+        } else {
+            ScratchStack st;
+            wavepersist_body<kStats>(sc, lds_nodes, st, job, samples, stats, err, work);
+        }
     } else {
-        wavepersist_body<kStats>(sc, sc.nodes, job, samples, stats, err, work);
+        ScratchStack st;
+        wavepersist_body<kStats>(sc, sc.nodes, st, job, samples, stats, err, work);
     }
 }
 
-template <bool kLds, int kBlock, int kMinWaves>
+template <int kLds, int kBlock, int kMinWaves>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
-                                       hipStream_t s) {
+                                       uint32_t stack_slots, hipStream_t s) {
     const uint32_t block = kBlock;
-    const size_t lds = kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0;
+    const size_t lds = (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
+                       (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves>
                             : k_trace_wavepersist<false, kLds, kBlock, kMinWaves>;
     int per_cu = 0, dev = 0, cus = 0;
@@ -215,18 +229,23 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     grid = std::max(1u, std::min(grid, (n_paths + block - 1) / block));
     e = hipMemsetAsync(work, 0, sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, s, sc, job, samples, stats, err, work);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, s, sc, job, samples, stats, err, work, stack_slots);
     return hipGetLastError();
 }
 
 // Register budget by launch bounds: waves/SIMD = 8 -> <= 64 VGPRs.
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
-                                    bool lds_nodes, uint32_t block, uint32_t min_waves, hipStream_t s) {
-#define MM_WP(B, W)                                                                                  \
-    if (block == B && min_waves == W)                                                                \
-        return lds_nodes ? launch_wavepersist_t<true, B, W>(sc, job, samples, stats, err, work, count_stats, s) \
-                         : launch_wavepersist_t<false, B, W>(sc, job, samples, stats, err, work, count_stats, s);
+                                    int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
+                                    hipStream_t s) {
+#define MM_WP(B, W)                                                                                          \
+    if (block == B && min_waves == W) {                                                                      \
+        if (lds_mode == 2)                                                                                   \
+            return launch_wavepersist_t<2, B, W>(sc, job, samples, stats, err, work, count_stats, stack_slots, s); \
+        if (lds_mode == 1)                                                                                   \
+            return launch_wavepersist_t<1, B, W>(sc, job, samples, stats, err, work, count_stats, stack_slots, s); \
+        return launch_wavepersist_t<0, B, W>(sc, job, samples, stats, err, work, count_stats, stack_slots, s);     \
+    }
     MM_WP(256, 1) MM_WP(256, 8) MM_WP(512, 1) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
 #undef MM_WP
     return hipErrorInvalidValue;

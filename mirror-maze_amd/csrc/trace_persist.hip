@@ -51,7 +51,7 @@ __device__ __forceinline__ void persist_body(const DevScene& sc, const Nodes& no
     bool fast = false, ovf = false;
     float t = kBig;
     uint32_t hit = 0, cur = 0, head = 0;
-    uint32_t stack[kStackMax];
+    ScratchStack stack;
     Counters c;
     uint32_t done_paths = 0;
 

@@ -104,7 +104,7 @@ __device__ __forceinline__ void extend_body(const DevScene& sc, const Nodes& nod
         const F3 d = F3{ws.dx[pid], ws.dy[pid], ws.dz[pid]};
         float t = kBig;
         uint32_t k = 0;
-        uint32_t stack[kStackMax];
+        ScratchStack stack;
         const bool ok = closest_hit<kStats>(sc, nodes, o, d, t, k, stack, c);
         if (kStats) c.rays++;
         ws.hit_t[pid] = t;

@@ -31,6 +31,8 @@ VARIANTS = {
 for _b, _w in ((256, 1), (256, 8), (512, 1), (512, 6), (512, 8), (1024, 1), (1024, 8)):
     VARIANTS[f"wp-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w)
     VARIANTS[f"wp-global-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=0, block=_b, mw=_w)
+    VARIANTS[f"wp-ldsstack-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=1)
+    VARIANTS[f"wp-lds-b{_b}-w{_w}"]["ls"] = 0
 for _b in (256, 512):
     for _th in (8, 16, 24, 32, 40, 48):
         VARIANTS[f"persist-lds-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, th=_th)
@@ -65,6 +67,8 @@ def main():
             r.set_option(MM_OPT_BLOCK, v["block"])
         if "persist" in v:
             r.set_option(MM_OPT_PERSIST, v["persist"])
+        if "ls" in v:
+            r.set_option(6, v["ls"])
         if "mw" in v:
             r.set_option(MM_OPT_MIN_WAVES, v["mw"])
         if "th" in v:

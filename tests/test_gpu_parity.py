@@ -105,7 +105,9 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "persist-lds": (1, {1: 1, 3: 1}),
     "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
     "persist-lds-t63-b256": (1, {1: 1, 3: 1, 4: 63, 2: 256}),
-    "wavepersist-lds": (1, {1: 1, 3: 2}),
+    "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0}),
+    "wavepersist-ldsstack": (1, {1: 1, 3: 2, 6: 1}),
+    "wavepersist-ldsstack-b512-w1": (1, {1: 1, 3: 2, 6: 1, 2: 512, 5: 1}),
     "wavepersist-lds-b512-w8": (1, {1: 1, 3: 2, 2: 512, 5: 8}),
     "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
     "wavefront": (2, {}),
