@@ -103,6 +103,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   2: wave-persistent megakernel, 64-path chunks (default) */
 #define MM_OPT_THRESHOLD   4   /* persistent kernel: traverse while > N lanes traverse (0..63) */
 #define MM_OPT_MIN_WAVES   5   /* wave-persistent kernel register budget: 1, 6 or 8 (default) waves/SIMD */
+#define MM_OPT_TRAVERSAL   7   /* wave-persistent kernel loop form: 0 if-if (default), 1 while-while,
+                                  8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
+#define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
 #define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 0 scratch (default) */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 

@@ -40,6 +40,7 @@ struct DevScene {
     uint32_t n_rects;
     uint32_t root_packed;     // count<<24 | left_first of node 0
     uint32_t fast_ok;         // scene coordinates inside the Markstein guard
+    const uint2* recs;        // 5 x uint2 per BVH slot: compact rect records (rect_compact.cpp)
 };
 
 // ---- IEEE helpers (the AIR intrinsics with their IEEE meaning) -------------

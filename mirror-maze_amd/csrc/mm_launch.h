@@ -41,7 +41,7 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
-                                    hipStream_t s);
+                                    int loop_form, hipStream_t s);
 
 struct PersistOpts {
     bool lds_nodes = true;

@@ -20,6 +20,10 @@
 
 using namespace mm;
 
+namespace mm {
+size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out);
+}
+
 struct mm_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -35,6 +39,8 @@ struct mm_ctx {
     bool stack16_ok = false;    // every node packs into 16 bits (count < 16, left_first < 4096)
     float4* d_geo = nullptr;
     float4* d_shade = nullptr;
+    uint2* d_recs = nullptr;    // compact leaf-ordered rect records
+    size_t n_fast_recs = 0;
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
     bool has_scene = false;
@@ -63,6 +69,8 @@ struct mm_ctx {
     // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
     int opt_persist = 2;         // 0 one thread per path, 1 lane refill, 2 wave-persistent
     uint32_t opt_min_waves = 8;  // wave-persistent launch bound (waves per SIMD)
+    int opt_ww = 0;              // traversal loop: 0 if-if, 1 while-while, 8/16/32 leaf batch
+    int opt_lds_rects = 1;       // compact rect records in LDS next to the BVH when they fit
     int opt_lds_stack = 0;       // u16 LDS stack: measured equal to scratch (profiles/r01_ab_ldsstack.txt)
     uint32_t opt_threshold = 32;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
@@ -101,6 +109,7 @@ DevScene dev_scene(const mm_ctx* c) {
     s.root_packed = c->root_packed;
     s.fast_ok = c->fast_ok ? 1u : 0u;
     s.geo = c->d_geo;
+    s.recs = c->d_recs;
     s.shade = c->d_shade;
     s.idx = c->d_idx;
     s.n_nodes = c->n_nodes;
@@ -110,8 +119,8 @@ DevScene dev_scene(const mm_ctx* c) {
 
 void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_nodes_ref); (void)hipFree(c->d_geo);
-    (void)hipFree(c->d_shade); (void)hipFree(c->d_idx);
-    c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
+    (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
+    c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
     c->has_scene = false;
 }
 
@@ -290,6 +299,12 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_threshold = (uint32_t)value;
             return MM_OK;
         case MM_OPT_LDS_STACK: c->opt_lds_stack = value != 0; return MM_OK;
+        case MM_OPT_TRAVERSAL:
+            if (value != 0 && value != 1 && value != 8 && value != 16 && value != 32)
+                return fail(c, MM_ERR_INVALID, "traversal loop form must be 0, 1, 8, 16 or 32");
+            c->opt_ww = value;
+            return MM_OK;
+        case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
         case MM_OPT_MIN_WAVES:
             if (value != 1 && value != 6 && value != 8) return fail(c, MM_ERR_INVALID, "min waves must be 1, 6 or 8");
             c->opt_min_waves = (uint32_t)value;
@@ -344,6 +359,11 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     HIPC(c, hipMalloc((void**)&c->d_geo, 4 * (size_t)n_rects * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_shade, 2 * (size_t)n_rects * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_idx, n_rects * sizeof(uint32_t)));
+    std::vector<uint32_t> recs;
+    c->n_fast_recs = n_rects < (1u << 20) ? build_compact_rects(rects, n_rects, idx, recs) : 0;
+    if (n_rects >= (1u << 20)) recs.assign(10 * (size_t)n_rects, 2u << 30);  // all SLOW (index does not fit)
+    HIPC(c, hipMalloc((void**)&c->d_recs, recs.size() * sizeof(uint32_t)));
+    HIPC(c, hipMemcpyAsync(c->d_recs, recs.data(), recs.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_rects, rects, n_rects * sizeof(mm_rect), hipMemcpyHostToDevice, c->stream));
     // mm_node is exactly two float4: (mn.xyz, mx.x) (mx.yz, left_first, count)
     HIPC(c, hipMemcpyAsync(c->d_nodes_ref, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
@@ -475,15 +495,22 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             launches += 1;
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
             const uint32_t block = c->opt_block ? c->opt_block : 1024u;
+            const bool inst = (block == 256 && c->opt_min_waves == 8) || (block == 512 && c->opt_min_waves >= 6) ||
+                              (block == 1024 && (c->opt_min_waves == 1 || c->opt_min_waves == 8));
+            if (!inst)
+                return fail(c, MM_ERR_UNSUPPORTED, "wave-persistent kernel: block/min-waves pair not instantiated "
+                                                   "(256/8, 512/6, 512/8, 1024/1, 1024/8)");
             const uint32_t slots = std::max(1u, c->depth);
             // keep 2 blocks of 1024 (or their equivalent) resident: <= 80 KB of LDS per block
             const size_t lds_total = 2 * (size_t)c->n_nodes * sizeof(float4) + (size_t)slots * block * 2;
             const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= (size_t)(160 * 1024) * block / 2048;
-            const int mode = lds_fits ? (stack_fits ? 2 : 1) : 0;
+            const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
+            const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * block / 2048;
+            const int mode = lds_fits ? (rects_fit ? 3 : (stack_fits ? 2 : 1)) : 0;
             HIPC(c, launch_trace_wavepersist(dev_scene(c), job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, mode, slots,
-                                             block, c->opt_min_waves, c->stream));
+                                             block, c->opt_min_waves, c->opt_ww, c->stream));
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
             PersistOpts po;
             po.lds_nodes = lds_fits;

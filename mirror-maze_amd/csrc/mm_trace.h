@@ -149,6 +149,64 @@ template <typename S> __device__ __forceinline__ uint32_t stack_cap(const S& st)
 template <> __device__ __forceinline__ uint32_t stack_cap<LdsStack16>(const LdsStack16& st) { return st.cap; }
 
 // ---------------------------------------------------------------------------
+// Scene views: where a traversal reads nodes and (optionally) the compact,
+// leaf-ordered rect records from (global memory or LDS).
+template <typename NodesT>
+struct NodeView {
+    NodesT nodes;
+    static constexpr bool kCompact = false;
+};
+template <typename NodesT, typename RecsT>
+struct CompactView {
+    NodesT nodes;
+    RecsT recs;  // 5 x uint2 per slot (rect_compact.cpp)
+    static constexpr bool kCompact = true;
+};
+template <typename N> __device__ __forceinline__ NodeView<N> view(N n) { return NodeView<N>{n}; }
+template <typename N, typename R> __device__ __forceinline__ CompactView<N, R> view(N n, R r) {
+    return CompactView<N, R>{n, r};
+}
+
+__device__ __forceinline__ float sel3(uint32_t a, F3 v) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+// ray_rect_intersect on a compact record (FAST kind) for a fast-guarded ray;
+// the derivation and the thresholds are in rect_compact.cpp.  SKIP records
+// can never hit; SLOW records run the general test from global memory.
+template <typename R>
+__device__ __forceinline__ void rect_test_compact(const DevScene& sc, const R& recs, uint32_t slot, const Ray& r,
+                                                  float& t, uint32_t& index) {
+    const uint2 w89 = recs[5 * slot + 4];
+    const uint32_t meta = w89.y, kind = meta >> 30;
+    if (kind == 1u) return;
+    const uint32_t k = meta & 0xFFFFFu;
+    if (kind == 2u) {
+        rect_test<true>(sc.geo, k, r, t, index);
+        return;
+    }
+    const uint2 w01 = recs[5 * slot + 0], w23 = recs[5 * slot + 1], w45 = recs[5 * slot + 2],
+                w67 = recs[5 * slot + 3];
+    const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
+    const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
+    const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
+    const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
+    if (x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) && x2 >= __uint_as_float(w67.y) &&
+        x2 <= __uint_as_float(w89.x) && a > 0.1f && a < t) {
+        t = a;
+        index = k;
+    }
+}
+
+template <bool kFast, typename V>
+__device__ __forceinline__ void leaf_tests(const DevScene& sc, const V& v, uint32_t lf, uint32_t cnt, const Ray& r,
+                                           float& t, uint32_t& index) {
+    if constexpr (V::kCompact && kFast) {
+        for (uint32_t i = 0; i < cnt; ++i) rect_test_compact(sc, v.recs, lf + i, r, t, index);
+    } else {
+        for (uint32_t i = 0; i < cnt; ++i) rect_test<kFast>(sc.geo, sc.idx[lf + i], r, t, index);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // intersect_bvh_iterative, production form.  Device node layout (built at
 // upload from the reference's 32-B BVHNode):
 //     a = (mn.x, mx.x, mn.y, mx.y)   b = (mn.z, mx.z, bits(packed), 0)
@@ -161,20 +219,20 @@ template <> __device__ __forceinline__ uint32_t stack_cap<LdsStack16>(const LdsS
 // (shaders.metal:126-155) on explicit state (cur, head, stack) and returns
 // true when the traversal is over (ovf set on stack overflow), so a caller
 // can interleave traversal steps of different rays (k_trace_persist).
-template <bool kFast, bool kStats, typename Nodes, typename Stack>
-__device__ __forceinline__ bool trav_step(const DevScene& sc, const Nodes& nodes, const Ray& r, float& t,
+template <bool kFast, bool kStats, typename V, typename Stack>
+__device__ __forceinline__ bool trav_step(const DevScene& sc, const V& v, const Ray& r, float& t,
                                           uint32_t& index, uint32_t& cur, uint32_t& head, Stack& stack,
                                           Counters& c, bool& ovf) {
     const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
     if (cnt > 0) {
-        for (uint32_t i = 0; i < cnt; ++i) rect_test<kFast>(sc.geo, sc.idx[lf + i], r, t, index);
+        leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
         if (kStats) c.rtests += cnt;
         if (head == 0) return true;
         cur = stack.pop(--head);
         return false;
     }
     if (kStats) c.visits++;
-    const float4 la = nodes[2 * lf], lb = nodes[2 * lf + 1], ra = nodes[2 * lf + 2], rb = nodes[2 * lf + 3];
+    const float4 la = v.nodes[2 * lf], lb = v.nodes[2 * lf + 1], ra = v.nodes[2 * lf + 2], rb = v.nodes[2 * lf + 3];
     float d1 = aabb_pairs<kFast>(la, lb, r, t);
     float d2 = aabb_pairs<kFast>(ra, rb, r, t);
     uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
@@ -195,12 +253,111 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const Nodes& nodes
     return false;
 }
 
-template <bool kFast, bool kStats, typename Nodes, typename Stack>
-__device__ __forceinline__ bool traverse(const DevScene& sc, const Nodes& nodes, const Ray& r, float& t,
+template <bool kFast, bool kStats, typename V, typename Stack>
+__device__ __forceinline__ bool traverse(const DevScene& sc, const V& v, const Ray& r, float& t,
                                          uint32_t& index, Stack& stack, Counters& c) {
     uint32_t cur = sc.root_packed, head = 0;
     bool ovf = false;
-    while (!trav_step<kFast, kStats>(sc, nodes, r, t, index, cur, head, stack, c, ovf)) {
+    while (!trav_step<kFast, kStats>(sc, v, r, t, index, cur, head, stack, c, ovf)) {
+    }
+    return !ovf;
+}
+
+// "while-while" form of the same traversal: each lane runs interior steps
+// until it reaches a leaf (or finishes), then the wave's leaves are processed
+// together.  Per lane the sequence of node visits, rect tests, pushes and
+// pops is exactly trav_step's (no speculation: a leaf is always tested
+// before the next node is visited), so results are identical; only the
+// interleaving of lanes' work inside a wave changes.
+template <bool kFast, bool kStats, typename V, typename Stack>
+__device__ __forceinline__ bool traverse_ww(const DevScene& sc, const V& v, const Ray& r, float& t,
+                                            uint32_t& index, Stack& stack, Counters& c) {
+    uint32_t cur = sc.root_packed, head = 0;
+    for (;;) {
+        // interior phase
+        bool done = false;
+        while ((cur >> 24) == 0) {
+            const uint32_t lf = cur & 0xFFFFFFu;
+            if (kStats) c.visits++;
+            const float4 la = v.nodes[2 * lf], lb = v.nodes[2 * lf + 1], ra = v.nodes[2 * lf + 2],
+                         rb = v.nodes[2 * lf + 3];
+            const float d1 = aabb_pairs<kFast>(la, lb, r, t);
+            const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
+            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+            const bool sw = d1 > d2;
+            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
+            const uint32_t pn = sw ? pr : pl, pf = sw ? pl : pr;
+            if (dn == kBig) {
+                if (head == 0) { done = true; break; }
+                cur = stack.pop(--head);
+            } else {
+                cur = pn;
+                if (df != kBig) {
+                    if (head >= stack_cap(stack)) return false;
+                    stack.push(head++, pf);
+                }
+            }
+        }
+        if (done) break;
+        // leaf phase
+        const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+        leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
+        if (kStats) c.rtests += cnt;
+        if (head == 0) break;
+        cur = stack.pop(--head);
+    }
+    return true;
+}
+
+// Leaf-batched form: every iteration the wave runs EITHER one interior step
+// for the lanes inside the tree OR the leaf tests for the lanes waiting at a
+// leaf -- the latter once at least `kBatch` lanes wait (or every unfinished
+// lane does).  A lane at a leaf does nothing until its leaf is tested, so per
+// lane the operation sequence is exactly trav_step's; only the interleaving
+// between lanes changes.  Avoids paying the leaf body (rect records, ~40 VALU)
+// in nearly every iteration as the if-if loop does (P(some lane of 64 at a
+// leaf) ~ 99 % at 1.47 leaf visits per 18.3 interior visits).
+template <bool kFast, bool kStats, uint32_t kBatch, typename V, typename Stack>
+__device__ __forceinline__ bool traverse_lb(const DevScene& sc, const V& v, const Ray& r, float& t,
+                                            uint32_t& index, Stack& stack, Counters& c) {
+    uint32_t cur = sc.root_packed, head = 0;
+    bool done = false, ovf = false;
+    for (;;) {
+        const bool at_leaf = !done && (cur >> 24) != 0;
+        const uint64_t live = __ballot(!done);
+        if (live == 0) break;
+        const uint64_t leaves = __ballot(at_leaf);
+        const bool do_leaves = leaves != 0 && (leaves == live || (uint32_t)__popcll(leaves) >= kBatch);
+        if (do_leaves) {
+            if (at_leaf) {
+                const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+                leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
+                if (kStats) c.rtests += cnt;
+                if (head == 0) done = true;
+                else cur = stack.pop(--head);
+            }
+        } else if (!done && !at_leaf) {
+            const uint32_t lf = cur & 0xFFFFFFu;
+            if (kStats) c.visits++;
+            const float4 la = v.nodes[2 * lf], lb = v.nodes[2 * lf + 1], ra = v.nodes[2 * lf + 2],
+                         rb = v.nodes[2 * lf + 3];
+            const float d1 = aabb_pairs<kFast>(la, lb, r, t);
+            const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
+            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+            const bool sw = d1 > d2;
+            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
+            const uint32_t pn = sw ? pr : pl, pf = sw ? pl : pr;
+            if (dn == kBig) {
+                if (head == 0) done = true;
+                else cur = stack.pop(--head);
+            } else {
+                cur = pn;
+                if (df != kBig) {
+                    if (head >= stack_cap(stack)) { ovf = true; done = true; }
+                    else stack.push(head++, pf);
+                }
+            }
+        }
     }
     return !ovf;
 }
@@ -245,12 +402,21 @@ __device__ __forceinline__ bool traverse_reference(const DevScene& sc, const Ray
 }
 
 // Closest hit for one ray: production traversal with the exact fallback.
-template <bool kStats, typename Nodes, typename Stack>
-__device__ __forceinline__ bool closest_hit(const DevScene& sc, const Nodes& nodes, F3 o, F3 d, float& t,
+// kWW selects the while-while loop structure.
+template <bool kStats, typename V, typename Stack, int kWW = 0>
+__device__ __forceinline__ bool closest_hit(const DevScene& sc, const V& v, F3 o, F3 d, float& t,
                                             uint32_t& index, Stack& stack, Counters& c) {
     const Ray r = make_ray(o, d);
-    if (sc.fast_ok && ray_fast_ok(r)) return traverse<true, kStats>(sc, nodes, r, t, index, stack, c);
-    return traverse<false, kStats>(sc, nodes, r, t, index, stack, c);
+    if constexpr (kWW >= 2) {
+        if (sc.fast_ok && ray_fast_ok(r)) return traverse_lb<true, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
+        return traverse_lb<false, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
+    } else if constexpr (kWW == 1) {
+        if (sc.fast_ok && ray_fast_ok(r)) return traverse_ww<true, kStats>(sc, v, r, t, index, stack, c);
+        return traverse_ww<false, kStats>(sc, v, r, t, index, stack, c);
+    } else {
+        if (sc.fast_ok && ray_fast_ok(r)) return traverse<true, kStats>(sc, v, r, t, index, stack, c);
+        return traverse<false, kStats>(sc, v, r, t, index, stack, c);
+    }
 }
 
 // Path state carried across bounces.
@@ -301,8 +467,8 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
 
 // Whole path (shaders.metal:302-344): returns sqrt(max(L, 0)).
 // kRef selects traverse_reference (MM_PIPE_REFERENCE).
-template <bool kStats, bool kRef, typename Nodes, typename Stack>
-__device__ __forceinline__ F3 trace_path(const DevScene& sc, const Nodes& nodes, F3 ori, F3 dir, uint32_t seed,
+template <bool kStats, bool kRef, typename V, typename Stack, int kWW = 0>
+__device__ __forceinline__ F3 trace_path(const DevScene& sc, const V& v, F3 ori, F3 dir, uint32_t seed,
                                          int bounce_limit, int mirror_limit, Stack& stack, Counters& c,
                                          bool& overflow) {
     PathState p;
@@ -315,7 +481,7 @@ __device__ __forceinline__ F3 trace_path(const DevScene& sc, const Nodes& nodes,
         uint32_t k = 0;
         bool ok;
         if constexpr (kRef) ok = traverse_reference<kStats>(sc, make_ray(p.ori, p.dir), t, k, stack, c);
-        else ok = closest_hit<kStats>(sc, nodes, p.ori, p.dir, t, k, stack, c);
+        else ok = closest_hit<kStats, V, Stack, kWW>(sc, v, p.ori, p.dir, t, k, stack, c);
         if (kStats) c.rays++;
         if (!ok) { overflow = true; break; }
         if (!shade_step(sc, p, t, k, mirror_limit)) break;

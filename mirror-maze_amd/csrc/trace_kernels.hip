@@ -77,7 +77,7 @@ __global__ __launch_bounds__(1024) void k_trace_chunks(DevScene sc, mm_uniform u
     ScratchStack stack;
     Counters c;
     bool overflow = false;
-    F3 s = trace_path<kStats, false>(sc, sc.nodes, ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
+    F3 s = trace_path<kStats, false>(sc, view(sc.nodes), ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
     if (overflow) atomicOr(err, 1u);
     // level 1..3: test[f] += test[f+1], += test[f+2], += test[f+4]
     s = s + F3{__shfl_xor(s.x, 1), __shfl_xor(s.y, 1), __shfl_xor(s.z, 1)};
@@ -135,10 +135,10 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
         bool overflow = false;
         F3 s;
         if constexpr (kLds)
-            s = trace_path<kStats, kRef>(sc, lds_nodes, ori, d, seed, (int)job.e.bounce_limit,
+            s = trace_path<kStats, kRef>(sc, view(lds_nodes), ori, d, seed, (int)job.e.bounce_limit,
                                          (int)job.e.mirror_limit, stack, c, overflow);
         else
-            s = trace_path<kStats, kRef>(sc, sc.nodes, ori, d, seed, (int)job.e.bounce_limit,
+            s = trace_path<kStats, kRef>(sc, view(sc.nodes), ori, d, seed, (int)job.e.bounce_limit,
                                          (int)job.e.mirror_limit, stack, c, overflow);
         if (overflow) atomicOr(err, 1u);
         samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
@@ -150,8 +150,8 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // each wave takes 64 consecutive paths at a time from a global counter and
 // traces them exactly like k_trace_mega, so no block waits for its slowest
 // wave before the CU can take more work.
-template <bool kStats, typename Nodes, typename Stack>
-__device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes& nodes, Stack& stack,
+template <bool kStats, int kWW, typename V, typename Stack>
+__device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v, Stack& stack,
                                                  const TileJob& job, float4* __restrict__ samples,
                                                  unsigned long long* stats, uint32_t* err, uint32_t* work) {
     const uint32_t spp = job.e.spp;
@@ -173,8 +173,8 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes
             uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
             const F3 d = jitter(primary_dir(job.u, px, py), seed);
             bool overflow = false;
-            const F3 s = trace_path<kStats, false>(sc, nodes, ori, d, seed, (int)job.e.bounce_limit,
-                                                   (int)job.e.mirror_limit, stack, c, overflow);
+            const F3 s = trace_path<kStats, false, V, Stack, kWW>(sc, v, ori, d, seed, (int)job.e.bounce_limit,
+                                                                  (int)job.e.mirror_limit, stack, c, overflow);
             if (overflow) atomicOr(err, 1u);
             samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
@@ -185,7 +185,7 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const Nodes
 
 // kLds: 0 nodes via L1/L2 + scratch stack, 1 nodes in LDS + scratch stack,
 // 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread).
-template <bool kStats, int kLds, int kBlock, int kMinWaves>
+template <bool kStats, int kLds, int kBlock, int kMinWaves, int kWW>
 __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
                                                                          float4* __restrict__ samples,
                                                                          unsigned long long* stats, uint32_t* err,
@@ -193,32 +193,39 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
     if constexpr (kLds > 0) {
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
+        uint2* lds_recs = reinterpret_cast<uint2*>(lds_nodes + 2 * sc.n_nodes);
+        if constexpr (kLds == 3)
+            for (uint32_t i = threadIdx.x; i < 5 * sc.n_rects; i += blockDim.x) lds_recs[i] = sc.recs[i];
         __syncthreads();
-        if constexpr (kLds == 2) {
+        if constexpr (kLds == 3) {
+            ScratchStack st;
+            wavepersist_body<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
+        } else if constexpr (kLds == 2) {
             LdsStack16 st;
-            st.base = reinterpret_cast<uint16_t*>(lds_nodes + 2 * sc.n_nodes) + threadIdx.x;
+            st.base = reinterpret_cast<uint16_t*>(lds_recs) + threadIdx.x;
             st.stride = blockDim.x;
             st.cap = stack_slots;
-            wavepersist_body<kStats>(sc, lds_nodes, st, job, samples, stats, err, work);
+            wavepersist_body<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         } else {
             ScratchStack st;
-            wavepersist_body<kStats>(sc, lds_nodes, st, job, samples, stats, err, work);
+            wavepersist_body<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         }
     } else {
         ScratchStack st;
-        wavepersist_body<kStats>(sc, sc.nodes, st, job, samples, stats, err, work);
+        wavepersist_body<kStats, kWW>(sc, view(sc.nodes), st, job, samples, stats, err, work);
     }
 }
 
-template <int kLds, int kBlock, int kMinWaves>
+template <int kLds, int kBlock, int kMinWaves, int kWW>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        uint32_t stack_slots, hipStream_t s) {
     const uint32_t block = kBlock;
     const size_t lds = (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
-                       (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0);
-    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves>
-                            : k_trace_wavepersist<false, kLds, kBlock, kMinWaves>;
+                       (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
+                       (kLds == 3 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
+    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves, kWW>
+                            : k_trace_wavepersist<false, kLds, kBlock, kMinWaves, kWW>;
     int per_cu = 0, dev = 0, cus = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
     if (e != hipSuccess) return e;
@@ -237,17 +244,17 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
-                                    hipStream_t s) {
-#define MM_WP(B, W)                                                                                          \
-    if (block == B && min_waves == W) {                                                                      \
-        if (lds_mode == 2)                                                                                   \
-            return launch_wavepersist_t<2, B, W>(sc, job, samples, stats, err, work, count_stats, stack_slots, s); \
-        if (lds_mode == 1)                                                                                   \
-            return launch_wavepersist_t<1, B, W>(sc, job, samples, stats, err, work, count_stats, stack_slots, s); \
-        return launch_wavepersist_t<0, B, W>(sc, job, samples, stats, err, work, count_stats, stack_slots, s);     \
-    }
-    MM_WP(256, 1) MM_WP(256, 8) MM_WP(512, 1) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
+                                    int loop_form, hipStream_t s) {
+#define MM_WP2(L, B, W, WW) \
+    if (lds_mode == L) return launch_wavepersist_t<L, B, W, WW>(sc, job, samples, stats, err, work, count_stats, stack_slots, s);
+#define MM_WP3(B, W, WW) \
+    if (loop_form == WW) { MM_WP2(3, B, W, WW) MM_WP2(2, B, W, WW) MM_WP2(1, B, W, WW) MM_WP2(0, B, W, WW) }
+#define MM_WP(B, W) \
+    if (block == B && min_waves == W) { MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 8) MM_WP3(B, W, 16) MM_WP3(B, W, 32) }
+    MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
 #undef MM_WP
+#undef MM_WP3
+#undef MM_WP2
     return hipErrorInvalidValue;
 }
 

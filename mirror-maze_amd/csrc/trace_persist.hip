@@ -29,8 +29,8 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-template <bool kStats, typename Nodes>
-__device__ __forceinline__ void persist_body(const DevScene& sc, const Nodes& nodes, const TileJob& job,
+template <bool kStats, typename V>
+__device__ __forceinline__ void persist_body(const DevScene& sc, const V& v, const TileJob& job,
                                              float4* __restrict__ samples, unsigned long long* stats,
                                              uint32_t* err, uint32_t* work, uint32_t threshold) {
     const uint32_t spp = job.e.spp;
@@ -130,8 +130,8 @@ __device__ __forceinline__ void persist_body(const DevScene& sc, const Nodes& no
             if (waiting && ntrav <= threshold) break;
             if (status == kTrav) {
                 bool fin;
-                if (fast) fin = trav_step<true, kStats>(sc, nodes, ray, t, hit, cur, head, stack, c, ovf);
-                else fin = trav_step<false, kStats>(sc, nodes, ray, t, hit, cur, head, stack, c, ovf);
+                if (fast) fin = trav_step<true, kStats>(sc, v, ray, t, hit, cur, head, stack, c, ovf);
+                else fin = trav_step<false, kStats>(sc, v, ray, t, hit, cur, head, stack, c, ovf);
                 if (fin) status = kShade;
             }
         }
@@ -169,9 +169,9 @@ __global__ __launch_bounds__(512) void k_trace_persist(DevScene sc, TileJob job,
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
         __syncthreads();
-        persist_body<kStats>(sc, lds_nodes, job, samples, stats, err, work, threshold);
+        persist_body<kStats>(sc, view(lds_nodes), job, samples, stats, err, work, threshold);
     } else {
-        persist_body<kStats>(sc, sc.nodes, job, samples, stats, err, work, threshold);
+        persist_body<kStats>(sc, view(sc.nodes), job, samples, stats, err, work, threshold);
     }
 }
 

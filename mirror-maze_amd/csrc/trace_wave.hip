@@ -92,8 +92,8 @@ __global__ __launch_bounds__(256) void k_wf_generate(TileJob job, WaveState ws, 
 }
 
 // ---------------------------------------------------------------------------
-template <bool kStats, typename Nodes>
-__device__ __forceinline__ void extend_body(const DevScene& sc, const Nodes& nodes, const WaveState& ws, int q,
+template <bool kStats, typename V>
+__device__ __forceinline__ void extend_body(const DevScene& sc, const V& v, const WaveState& ws, int q,
                                             unsigned long long* stats) {
     const uint32_t n_in = ws.counters[q];
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -105,7 +105,7 @@ __device__ __forceinline__ void extend_body(const DevScene& sc, const Nodes& nod
         float t = kBig;
         uint32_t k = 0;
         ScratchStack stack;
-        const bool ok = closest_hit<kStats>(sc, nodes, o, d, t, k, stack, c);
+        const bool ok = closest_hit<kStats>(sc, v, o, d, t, k, stack, c);
         if (kStats) c.rays++;
         ws.hit_t[pid] = t;
         ws.hit_i[pid] = ok ? k : kHitOverflow;
@@ -134,9 +134,9 @@ __global__ __launch_bounds__(512) void k_wf_extend(DevScene sc, WaveState ws, in
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
         __syncthreads();
-        extend_body<kStats>(sc, lds_nodes, ws, q, stats);
+        extend_body<kStats>(sc, view(lds_nodes), ws, q, stats);
     } else {
-        extend_body<kStats>(sc, sc.nodes, ws, q, stats);
+        extend_body<kStats>(sc, view(sc.nodes), ws, q, stats);
     }
 }
 

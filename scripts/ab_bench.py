@@ -28,11 +28,18 @@ VARIANTS = {
     "wave-global": dict(pipe=2, lds=0),
     "wave-b256": dict(pipe=2, block=256),
 }
-for _b, _w in ((256, 1), (256, 8), (512, 1), (512, 6), (512, 8), (1024, 1), (1024, 8)):
+for _b, _w in ((512, 6), (512, 8), (1024, 1), (1024, 8)):
+    for _k in (8, 16, 32):
+        VARIANTS[f"lb{_k}-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1, ww=_k)
+        VARIANTS[f"lb{_k}-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=0, ww=_k)
+    VARIANTS[f"ww-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, ww=1)
+    VARIANTS[f"ww-ldsstack-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=1, ww=1)
     VARIANTS[f"wp-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w)
     VARIANTS[f"wp-global-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=0, block=_b, mw=_w)
     VARIANTS[f"wp-ldsstack-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=1)
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["ls"] = 0
+    VARIANTS[f"wp-lds-b{_b}-w{_w}"]["lr"] = 0
+    VARIANTS[f"wp-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1)
 for _b in (256, 512):
     for _th in (8, 16, 24, 32, 40, 48):
         VARIANTS[f"persist-lds-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, th=_th)
@@ -67,6 +74,10 @@ def main():
             r.set_option(MM_OPT_BLOCK, v["block"])
         if "persist" in v:
             r.set_option(MM_OPT_PERSIST, v["persist"])
+        if "lr" in v:
+            r.set_option(8, v["lr"])
+        if "ww" in v:
+            r.set_option(7, v["ww"])
         if "ls" in v:
             r.set_option(6, v["ls"])
         if "mw" in v:

@@ -105,9 +105,15 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "persist-lds": (1, {1: 1, 3: 1}),
     "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
     "persist-lds-t63-b256": (1, {1: 1, 3: 1, 4: 63, 2: 256}),
-    "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0}),
-    "wavepersist-ldsstack": (1, {1: 1, 3: 2, 6: 1}),
-    "wavepersist-ldsstack-b512-w1": (1, {1: 1, 3: 2, 6: 1, 2: 512, 5: 1}),
+    "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0, 8: 0}),
+    "wavepersist-ldsrects": (1, {1: 1, 3: 2, 8: 1}),
+    "wavepersist-ldsrects-b512-w6": (1, {1: 1, 3: 2, 8: 1, 2: 512, 5: 6}),
+    "wavepersist-ldsstack": (1, {1: 1, 3: 2, 6: 1, 8: 0}),
+    "wavepersist-ldsstack-b512-w6": (1, {1: 1, 3: 2, 6: 1, 2: 512, 5: 6}),
+    "whilewhile-lds": (1, {1: 1, 3: 2, 7: 1}),
+    "leafbatch16-ldsrects": (1, {1: 1, 3: 2, 7: 16, 8: 1}),
+    "leafbatch8-global": (1, {1: 0, 3: 2, 7: 8}),
+    "whilewhile-global-ldsstack": (1, {1: 0, 3: 2, 7: 1, 6: 1}),
     "wavepersist-lds-b512-w8": (1, {1: 1, 3: 2, 2: 512, 5: 8}),
     "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
     "wavefront": (2, {}),
@@ -144,6 +150,32 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
         assert (st.rays, st.node_visits, st.rect_tests, st.paths) == \
                (rst.rays, rst.node_visits, rst.rect_tests, rst.paths)
     ren.close()
+
+
+@pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects"])
+def test_small_full_frames_bit_exact(gpu, pipe):
+    """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
+    closest-hit queries per pipeline against the oracle, so rare boundary
+    cases of the exact-division and threshold tests get exercised."""
+    from mirror_maze import Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(32)
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    p, opts = PIPES[pipe]
+    r.set_pipeline(p)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload_scene(s)
+    u = default_uniform(256, 144, 0)
+    for frame in range(3):
+        e = make_ext(8, 8, 8, frame=frame)
+        got, _ = r.trace_tile(u, e, 0, 0, 256, 144)
+        ref, _ = o.trace_tile(u, e, 0, 0, 256, 144)
+        bad = (_bits(got.cpu().numpy()) != _bits(ref)).any(axis=-1)
+        assert not bad.any(), f"frame {frame}: {int(bad.sum())} pixels differ"
+    r.close()
 
 
 def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
