@@ -10,6 +10,7 @@
  *                     460,467,494,501,303-305
  *   mm_maze_build     Kruskal maze + wall runs + planes   src/main.rs:356-586
  *   mm_bvh_build      SAH BVH                              src/main.rs:74-263
+ *   mm_bvh_build_ex   same, explicit split-search method   src/main.rs:102-211
  *   mm_camera_default camera + calculate_quaternion        src/main.rs:732-755,
  *                                                          src/maths.rs:139-156
  *   mm_chunks_*       chunk scheduler gen_pixels/random_pixels
@@ -66,9 +67,19 @@ int  mm_scene_build(uint32_t maze_n, uint64_t seed, mm_scene** out);
 void mm_scene_free(mm_scene* s);
 
 /* SAH BVH over n rects (src/main.rs:247-263).  nodes_out must hold 2n-1
- * nodes, idx_out n entries.  *n_nodes receives the number used. */
+ * nodes, idx_out n entries.  *n_nodes receives the number used.  The split
+ * search is the sorted sweep (MM_BVH_SWEEP): same tree as the reference. */
 int  mm_bvh_build(const mm_rect* rects, uint32_t n, mm_node* nodes_out,
                   uint32_t* n_nodes, uint32_t* idx_out);
+/* Split-search methods; both produce the reference's node array bit for bit.
+ *   MM_BVH_SWEEP       sort each axis once per node, prefix/suffix boxes:
+ *                      O(n log n) per node (N=64 maze: milliseconds)
+ *   MM_BVH_EXHAUSTIVE  the reference's loop, every candidate re-scans the node
+ *                      (src/main.rs:110-125, 180-211): O(n^2) per node */
+#define MM_BVH_SWEEP      0
+#define MM_BVH_EXHAUSTIVE 1
+int  mm_bvh_build_ex(const mm_rect* rects, uint32_t n, mm_node* nodes_out,
+                     uint32_t* n_nodes, uint32_t* idx_out, int method);
 /* Max depth of the tree (root = 0) — the traversal stack never holds more. */
 uint32_t mm_bvh_depth(const mm_node* nodes, uint32_t n_nodes);
 

@@ -44,14 +44,17 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     int loop_form, hipStream_t s);
 
 struct PersistOpts {
-    bool lds_nodes = true;
-    uint32_t block = 512;
+    int lds_mode = 1;          // 0 nodes via cache, 1 nodes in LDS, 3 nodes + compact rects in LDS
+    uint32_t block = 1024;
+    uint32_t min_waves = 8;    // launch-bounds occupancy target (waves per SIMD)
     uint32_t threshold = 32;   // keep stepping traversals while > threshold lanes traverse
-    uint32_t grid_mult = 1;    // blocks = occupancy * CUs * grid_mult
 };
 
-// Throughput mode, persistent megakernel (trace_persist.hip).  `work` is a
-// device u32 path counter (zeroed by the launcher).
+// (block, min_waves) pairs launch_trace_persist is compiled for.
+bool persist_instantiated(uint32_t block, uint32_t min_waves);
+
+// Throughput mode, lane-refill persistent megakernel (trace_persist.hip).
+// `work` is a device u32 path counter (zeroed by the launcher).
 hipError_t launch_trace_persist(const DevScene& sc, const TileJob& job, float4* samples,
                                 unsigned long long* stats_dev, uint32_t* err, uint32_t* work, bool count_stats,
                                 const PersistOpts& o, hipStream_t s);

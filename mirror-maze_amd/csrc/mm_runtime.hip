@@ -513,8 +513,14 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                                              block, c->opt_min_waves, c->opt_ww, c->stream));
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
             PersistOpts po;
-            po.lds_nodes = lds_fits;
-            po.block = c->opt_block ? c->opt_block : 512u;
+            po.block = c->opt_block ? c->opt_block : 1024u;
+            po.min_waves = c->opt_min_waves;
+            if (!persist_instantiated(po.block, po.min_waves))
+                return fail(c, MM_ERR_UNSUPPORTED, "lane-refill kernel: block/min-waves pair not instantiated "
+                                                   "(1024/8, 1024/1, 512/6)");
+            const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
+            const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * po.block / 2048;
+            po.lds_mode = lds_fits ? (rects_fit ? 3 : 1) : 0;
             po.threshold = c->opt_threshold;
             HIPC(c, launch_trace_persist(dev_scene(c), job, c->d_samples, c->d_aux,
                                          reinterpret_cast<uint32_t*>(c->d_aux + 4),

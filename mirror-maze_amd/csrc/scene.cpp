@@ -6,6 +6,7 @@
 // contracts to FMA and evaluates left to right).
 #include "mm_scene.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -109,6 +110,7 @@ struct BvhBuilder {
     std::vector<F3> centers;
     std::vector<uint32_t> idx;
     std::vector<mm_node> nodes;
+    bool exhaustive = false;  // the reference's O(n^2) candidate loop (MM_BVH_EXHAUSTIVE)
 
     static mm_node new_node(uint32_t lf, uint32_t count) {
         mm_node n;
@@ -136,17 +138,70 @@ struct BvhBuilder {
         cost = cost + (float)rc * rb.area();
         return cost > 0.0f ? cost : 1e30f;  // NaN (0*inf) also maps to 1e30
     }
+    // The same candidate loop in O(n log n) per node.  eval_sah's left set for
+    // candidate c on `axis` is {p : center_p[axis] < c}: a prefix of the
+    // primitives sorted by center.  Growing a box is min/max, so the prefix
+    // (suffix) box over the sorted order has the bounds eval_sah accumulates in
+    // index order — up to the sign of a zero bound, which cannot change the
+    // value of a cost — and the cost expression is evaluated with eval_sah's
+    // operations on the same counts.  Candidates are visited in eval order with
+    // the same `<=`, so the chosen (axis, pos) is identical.  Returns false
+    // (caller runs the exhaustive loop) if a center is NaN.
+    bool sweep_split(const mm_node& self, int& best_axis, float& best_pos, float& best_cost) const {
+        const uint32_t n = self.count, lf = self.left_first;
+        std::vector<Box> pbox(n);
+        for (uint32_t i = 0; i < n; ++i) pbox[i].grow_plane(planes[idx[lf + i]]);
+        std::vector<uint32_t> ord(n);
+        std::vector<float> keys(n), lterm(n + 1), rterm(n + 1);
+        for (int axis = 0; axis <= 2; ++axis) {
+            for (uint32_t i = 0; i < n; ++i) {
+                keys[i] = idx3(centers[idx[lf + i]], axis);
+                if (std::isnan(keys[i])) return false;
+                ord[i] = i;
+            }
+            std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+            Box acc;
+            lterm[0] = 0.0f * acc.area();
+            for (uint32_t k = 1; k <= n; ++k) {
+                const Box& b = pbox[ord[k - 1]];
+                acc.mn = F3{std::fmin(acc.mn.x, b.mn.x), std::fmin(acc.mn.y, b.mn.y), std::fmin(acc.mn.z, b.mn.z)};
+                acc.mx = F3{std::fmax(acc.mx.x, b.mx.x), std::fmax(acc.mx.y, b.mx.y), std::fmax(acc.mx.z, b.mx.z)};
+                lterm[k] = (float)k * acc.area();
+            }
+            acc = Box();
+            rterm[n] = 0.0f * acc.area();
+            for (uint32_t k = n; k-- > 0;) {
+                const Box& b = pbox[ord[k]];
+                acc.mn = F3{std::fmin(acc.mn.x, b.mn.x), std::fmin(acc.mn.y, b.mn.y), std::fmin(acc.mn.z, b.mn.z)};
+                acc.mx = F3{std::fmax(acc.mx.x, b.mx.x), std::fmax(acc.mx.y, b.mx.y), std::fmax(acc.mx.z, b.mx.z)};
+                rterm[k] = (float)(n - k) * acc.area();
+            }
+            std::vector<float> sorted(n);
+            for (uint32_t k = 0; k < n; ++k) sorted[k] = keys[ord[k]];
+            for (uint32_t i = 0; i < n; ++i) {
+                const float cand = keys[i];
+                const uint32_t lc = (uint32_t)(std::lower_bound(sorted.begin(), sorted.end(), cand) - sorted.begin());
+                float cost = lterm[lc];
+                cost = cost + rterm[lc];
+                cost = cost > 0.0f ? cost : 1e30f;
+                if (cost <= best_cost) { best_cost = cost; best_pos = cand; best_axis = axis; }
+            }
+        }
+        return true;
+    }
     // subdivide (main.rs:102-179).  `self` is the node value held by the
     // caller; children are pushed, recursed, then written back.
     void subdivide(mm_node& self) {
         if (self.count == 1) return;
         float best_pos = 0.0f, best_cost = 1e30f;
         int best_axis = 6;
-        for (int axis = 0; axis <= 2; ++axis) {
-            for (uint32_t i = self.left_first; i < self.left_first + self.count; ++i) {
-                float cand = idx3(plane_center(planes[idx[i]]), axis);
-                float cost = eval_sah(self, axis, cand);
-                if (cost <= best_cost) { best_cost = cost; best_pos = cand; best_axis = axis; }
+        if (exhaustive || !sweep_split(self, best_axis, best_pos, best_cost)) {
+            for (int axis = 0; axis <= 2; ++axis) {
+                for (uint32_t i = self.left_first; i < self.left_first + self.count; ++i) {
+                    float cand = idx3(plane_center(planes[idx[i]]), axis);
+                    float cost = eval_sah(self, axis, cand);
+                    if (cost <= best_cost) { best_cost = cost; best_pos = cand; best_axis = axis; }
+                }
             }
         }
         F3 diag = sub3(F3{self.mx[0], self.mx[1], self.mx[2]}, F3{self.mn[0], self.mn[1], self.mn[2]});
@@ -294,10 +349,17 @@ uint32_t mm_rng_gen_range_u32(mm_rng* r, uint32_t lo, uint32_t hi) {
 
 int mm_bvh_build(const mm_rect* rects, uint32_t n, mm_node* nodes_out, uint32_t* n_nodes,
                  uint32_t* idx_out) {
+    return mm_bvh_build_ex(rects, n, nodes_out, n_nodes, idx_out, MM_BVH_SWEEP);
+}
+
+int mm_bvh_build_ex(const mm_rect* rects, uint32_t n, mm_node* nodes_out, uint32_t* n_nodes,
+                    uint32_t* idx_out, int method) {
     if (!rects || !nodes_out || !n_nodes || !idx_out || n == 0) return MM_ERR_INVALID;
+    if (method != MM_BVH_SWEEP && method != MM_BVH_EXHAUSTIVE) return MM_ERR_INVALID;
     try {
         BvhBuilder b;
         b.planes = rects;
+        b.exhaustive = method == MM_BVH_EXHAUSTIVE;
         b.nodes.reserve(2 * (size_t)n - 1);
         b.centers.resize(n);
         b.idx.resize(n);

@@ -35,6 +35,7 @@ MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE = 0x1, 0x2
 MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2, 3
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_THRESHOLD, MM_OPT_MIN_WAVES, MM_OPT_LDS_STACK = 1, 2, 3, 4, 5, 6
 MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS = 7, 8
+MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
 
 
@@ -109,6 +110,7 @@ EXPORTS = {
     "mm_scene_build": (C.c_int, [C.c_uint32, C.c_uint64, C.POINTER(C.POINTER(mm_scene))]),
     "mm_scene_free": (None, [C.POINTER(mm_scene)]),
     "mm_bvh_build": (C.c_int, [P, C.c_uint32, P, C.POINTER(C.c_uint32), P]),
+    "mm_bvh_build_ex": (C.c_int, [P, C.c_uint32, P, C.POINTER(C.c_uint32), P, C.c_int]),
     "mm_bvh_depth": (C.c_uint32, [P, C.c_uint32]),
     "mm_calculate_quaternion": (None, [P, P]),
     "mm_uniform_default": (None, [C.c_float, C.c_float, C.c_uint32, C.POINTER(mm_uniform)]),

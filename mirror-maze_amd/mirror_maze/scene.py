@@ -60,14 +60,17 @@ class Scene:
             L.mm_scene_free(p)
 
     @staticmethod
-    def bvh(rects: np.ndarray):
-        """Rebuild the SAH BVH for an arbitrary (P, 12) float32 rect array."""
+    def bvh(rects: np.ndarray, method: int = _lib.MM_BVH_SWEEP):
+        """Rebuild the SAH BVH for an arbitrary (P, 12) float32 rect array.
+
+        method: MM_BVH_SWEEP (sorted sweep, default) or MM_BVH_EXHAUSTIVE (the
+        reference's O(n^2) candidate loop); both give the same tree."""
         rects = np.ascontiguousarray(rects, dtype=np.float32)
         P = rects.shape[0]
         nodes = np.zeros(2 * P - 1, dtype=NODE_DTYPE)
         idx = np.zeros(P, dtype=np.uint32)
         n = C.c_uint32()
-        check(lib().mm_bvh_build(rects.ctypes.data, P, nodes.ctypes.data, C.byref(n), idx.ctypes.data))
+        check(lib().mm_bvh_build_ex(rects.ctypes.data, P, nodes.ctypes.data, C.byref(n), idx.ctypes.data, method))
         return nodes[: n.value].copy(), idx
 
 

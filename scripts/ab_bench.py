@@ -40,10 +40,11 @@ for _b, _w in ((512, 6), (512, 8), (1024, 1), (1024, 8)):
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["ls"] = 0
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["lr"] = 0
     VARIANTS[f"wp-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1)
-for _b in (256, 512):
-    for _th in (8, 16, 24, 32, 40, 48):
-        VARIANTS[f"persist-lds-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, th=_th)
-        VARIANTS[f"persist-global-b{_b}-t{_th}"] = dict(pipe=1, persist=1, lds=0, block=_b, th=_th)
+for _b, _w in ((512, 6), (1024, 1), (1024, 8)):
+    for _th in (0, 8, 16, 24, 32, 40, 48):
+        VARIANTS[f"persist-lds-b{_b}-w{_w}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, mw=_w, th=_th, lr=0)
+        VARIANTS[f"persist-ldsrec-b{_b}-w{_w}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, mw=_w, th=_th, lr=1)
+        VARIANTS[f"persist-global-b{_b}-w{_w}-t{_th}"] = dict(pipe=1, persist=1, lds=0, block=_b, mw=_w, th=_th)
 
 
 def main():

@@ -102,9 +102,11 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "mega-global": (1, {1: 0, 3: 0}),
     "mega-lds": (1, {1: 1, 3: 0}),
     "mega-lds-b1024": (1, {1: 1, 2: 1024, 3: 0}),
-    "persist-lds": (1, {1: 1, 3: 1}),
+    "persist-lds": (1, {1: 1, 3: 1, 8: 0}),
+    "persist-ldsrects": (1, {1: 1, 3: 1, 8: 1}),
     "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
-    "persist-lds-t63-b256": (1, {1: 1, 3: 1, 4: 63, 2: 256}),
+    "persist-ldsrects-t63-b512-w6": (1, {1: 1, 3: 1, 4: 63, 2: 512, 5: 6}),
+    "persist-lds-t16-b1024-w1": (1, {1: 1, 3: 1, 4: 16, 2: 1024, 5: 1, 8: 0}),
     "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0, 8: 0}),
     "wavepersist-ldsrects": (1, {1: 1, 3: 2, 8: 1}),
     "wavepersist-ldsrects-b512-w6": (1, {1: 1, 3: 2, 8: 1, 2: 512, 5: 6}),

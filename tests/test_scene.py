@@ -140,3 +140,41 @@ def test_chunk_scheduler_pops_and_refills():
     assert seen[:, 0].max() == 1020 and seen[:, 1].max() == 764 and np.all(seen % 4 == 0)
     again = cs.next(768)  # refill from the original shuffled list: same order as cycle 1
     assert np.array_equal(again, seen[:768])
+
+
+def _same_tree(a, b):
+    (na, ia), (nb, ib) = a, b
+    assert len(na) == len(nb)
+    assert np.array_equal(ia, ib)
+    assert np.array_equal(na.view(np.uint8), nb.view(np.uint8))  # every bit of every node
+
+
+@pytest.mark.parametrize("n", [4, 10, 32, 64])
+def test_bvh_sweep_equals_exhaustive_maze(n):
+    """The O(n log n) sweep split search builds the reference's tree bit for bit
+    (the exhaustive form is the reference's loop, src/main.rs:110-125, 180-211)."""
+    from mirror_maze import Scene
+    from mirror_maze._lib import MM_BVH_EXHAUSTIVE, MM_BVH_SWEEP
+
+    s = _build(n)
+    sweep = Scene.bvh(s.rects, MM_BVH_SWEEP)
+    _same_tree(sweep, (s.nodes, s.idx))
+    _same_tree(sweep, Scene.bvh(s.rects, MM_BVH_EXHAUSTIVE))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_bvh_sweep_equals_exhaustive_adversarial(seed):
+    """Ties everywhere: coordinates on a coarse grid (equal centers and equal
+    costs), zero-length rects, signed zeros, huge and tiny extents."""
+    from mirror_maze import Scene
+    from mirror_maze._lib import MM_BVH_EXHAUSTIVE, MM_BVH_SWEEP
+
+    rng = np.random.default_rng(seed)
+    P = int(rng.integers(2, 300))
+    r = rng.integers(-4, 5, size=(P, 12)).astype(np.float32) * np.float32(2.5)
+    r[rng.random(P) < 0.2, 3:6] = 0.0                       # zero-length v
+    r[rng.random((P, 12)) < 0.05] = -0.0                    # signed zeros
+    if seed % 2:
+        r[rng.random(P) < 0.1, 0] = np.float32(3e20)        # far outliers
+        r[rng.random(P) < 0.1, 6:9] *= np.float32(1e-6)     # tiny extents
+    _same_tree(Scene.bvh(r, MM_BVH_SWEEP), Scene.bvh(r, MM_BVH_EXHAUSTIVE))
