@@ -36,6 +36,8 @@ CONFIGS = {
     "c2": (16, 1920, 1080, 1, 4, 15, "C2: 16x16 maze, 1920x1080, 1 spp, 4 bounces"),
     "c3": (32, 1920, 1080, 8, 8, 8, "C3: 32x32 maze, 1920x1080, 8 spp, 8 mirror bounces"),
     "c4": (32, 3840, 2160, 16, 8, 15, "C4: 32x32 maze, 3840x2160, 16 spp, 8 bounces"),
+    "c5": (64, 3840, 2160, 64, 16, 16, "C5 frame: 64x64 maze, 3840x2160, 64 spp, 16/16 bounces"),
+    "c5s": (64, 1920, 1080, 8, 16, 16, "C5 scene at C3 size: 64x64 maze, 1920x1080, 8 spp, 16/16 bounces"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, non-packed fp32 ops

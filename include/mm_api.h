@@ -107,6 +107,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
 #define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
 #define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 0 scratch (default) */
+#define MM_OPT_LDS_SPLIT   9   /* wave-persistent kernel, BVH larger than the LDS budget: cache the top of
+                                  the (breadth-first) node array in LDS, rest via L1/L2.
+                                  0 off, 1 auto size (default), >1: always use a cache of this many KB */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Wait for all work queued by this context. */

@@ -32,11 +32,12 @@ constexpr int kStackMax = 50;     // shaders.metal:123
 // Shade record: s0 = (color.rgb, is_mirror), s1 = emission (rgba).
 struct DevScene {
     const float4* nodes;      // 2 * n_nodes, production layout
-    const float4* nodes_ref;  // 2 * n_nodes, reference layout
+    const float4* nodes_ref;  // 2 * n_nodes_ref, reference layout
     const float4* geo;        // 4 * n_rects
     const float4* shade;      // 2 * n_rects
     const uint32_t* idx;      // n_rects
-    uint32_t n_nodes;
+    uint32_t n_nodes;         // production array length in nodes (breadth-first pairs)
+    uint32_t n_lds_f4;        // float4s of `nodes` staged in LDS by split-cache kernels
     uint32_t n_rects;
     uint32_t root_packed;     // count<<24 | left_first of node 0
     uint32_t fast_ok;         // scene coordinates inside the Markstein guard

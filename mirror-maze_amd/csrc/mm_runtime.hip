@@ -64,6 +64,7 @@ struct mm_ctx {
     uint32_t last_launches = 0;
     int pipe = MM_PIPE_AUTO;
     bool opt_lds = true;
+    uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto size, else KB
     uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
     // Megakernel form (measured on C3, profiles/r01_ab_*.txt): wave-persistent
     // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
@@ -305,6 +306,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
+        case MM_OPT_LDS_SPLIT:
+            if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
+            c->opt_lds_split = (uint32_t)value;
+            return MM_OK;
         case MM_OPT_MIN_WAVES:
             if (value != 1 && value != 6 && value != 8) return fail(c, MM_ERR_INVALID, "min waves must be 1, 6 or 8");
             c->opt_min_waves = (uint32_t)value;
@@ -327,19 +332,44 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     uint32_t depth = 0;
     int rc = check_tree(nodes, n_nodes, idx, n_rects, why, &depth);
     if (rc != MM_OK) return fail(c, rc, "mm_upload_scene: " + why);
-    // production node layout: a = (mn.x, mx.x, mn.y, mx.y), b = (mn.z, mx.z, packed, 0),
-    // packed = count << 24 | left_first
-    std::vector<float4> packed(2 * (size_t)n_nodes);
-    for (uint32_t i = 0; i < n_nodes; ++i) {
-        const mm_node& nd = nodes[i];
-        if (nd.count >= 256u || nd.left_first >= (1u << 24))
+    // Production node layout: a = (mn.x, mx.x, mn.y, mx.y), b = (mn.z, mx.z, packed, 0),
+    // packed = count << 24 | left_first.  Child pairs are renumbered
+    // breadth-first from the root's pair, which lands at node 2 (nodes 0-1 are
+    // never read: the root is not tested, shaders.metal:123-125), so every pair
+    // is one aligned 64-B line and a prefix of the array is the top of the tree
+    // (the split LDS cache of mm_trace.h).  Only traversal order matters to the
+    // result, and it depends on distances, not on indices.
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        if (nodes[i].count >= 256u || nodes[i].left_first >= (1u << 24))
             return fail(c, MM_ERR_UNSUPPORTED, "mm_upload_scene: leaf with >= 256 planes or index >= 2^24");
-        uint32_t pk = (nd.count << 24) | nd.left_first;
-        float pkf;
-        std::memcpy(&pkf, &pk, 4);
-        packed[2 * i] = make_float4(nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1]);
-        packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
-    }
+    std::vector<uint32_t> pair_old;  // old index of each pair's left node, breadth-first
+    if (nodes[0].count == 0) pair_old.push_back(nodes[0].left_first);
+    for (size_t q = 0; q < pair_old.size(); ++q)
+        for (uint32_t k = 0; k < 2; ++k) {
+            const mm_node& nd = nodes[pair_old[q] + k];
+            if (nd.count == 0) pair_old.push_back(nd.left_first);
+        }
+    std::vector<uint32_t> pair_new(n_nodes, 0);  // old left index -> new left index
+    for (size_t q = 0; q < pair_old.size(); ++q) pair_new[pair_old[q]] = 2 + 2 * (uint32_t)q;
+    if (2 + 2 * pair_old.size() >= (1u << 24))
+        return fail(c, MM_ERR_UNSUPPORTED, "mm_upload_scene: node index >= 2^24");
+    auto pack = [&](const mm_node& nd) {
+        return nd.count > 0 ? (nd.count << 24) | nd.left_first : pair_new[nd.left_first];
+    };
+    const uint32_t n_prod = 2 + 2 * (uint32_t)pair_old.size();
+    std::vector<float4> packed(2 * (size_t)n_prod, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    bool stack16 = true;
+    for (size_t q = 0; q < pair_old.size(); ++q)
+        for (uint32_t k = 0; k < 2; ++k) {
+            const mm_node& nd = nodes[pair_old[q] + k];
+            const uint32_t pk = pack(nd);
+            if ((pk >> 24) >= 16u || (pk & 0xFFFFFFu) >= 4096u) stack16 = false;
+            float pkf;
+            std::memcpy(&pkf, &pk, 4);
+            const size_t i = 2 + 2 * q + k;
+            packed[2 * i] = make_float4(nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1]);
+            packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
+        }
     bool fast = true;
     for (uint32_t i = 0; i < n_nodes && fast; ++i)
         for (int a = 0; a < 3; ++a) fast = fast && coord_ok(nodes[i].mn[a]) && coord_ok(nodes[i].mx[a]);
@@ -354,7 +384,7 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         shade[2 * k + 1] = make_float4(emission[4 * k], emission[4 * k + 1], emission[4 * k + 2], emission[4 * k + 3]);
     }
     HIPC(c, hipMalloc((void**)&c->d_rects, n_rects * sizeof(mm_rect)));
-    HIPC(c, hipMalloc((void**)&c->d_nodes, n_nodes * sizeof(mm_node)));
+    HIPC(c, hipMalloc((void**)&c->d_nodes, packed.size() * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_nodes_ref, n_nodes * sizeof(mm_node)));
     HIPC(c, hipMalloc((void**)&c->d_geo, 4 * (size_t)n_rects * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_shade, 2 * (size_t)n_rects * sizeof(float4)));
@@ -373,12 +403,10 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));  // host arrays may be freed on return
     c->n_rects = n_rects;
-    c->n_nodes = n_nodes;
-    c->root_packed = (nodes[0].count << 24) | nodes[0].left_first;
+    c->n_nodes = n_prod;
+    c->root_packed = pack(nodes[0]);
     c->depth = depth;
-    c->stack16_ok = true;
-    for (uint32_t i = 0; i < n_nodes; ++i)
-        if (nodes[i].count >= 16u || nodes[i].left_first >= 4096u) c->stack16_ok = false;
+    c->stack16_ok = stack16 && (c->root_packed >> 24) < 16u && (c->root_packed & 0xFFFFFFu) < 4096u;
     c->fast_ok = fast;
     c->has_scene = true;
     return MM_OK;
@@ -506,8 +534,17 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= (size_t)(160 * 1024) * block / 2048;
             const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
             const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * block / 2048;
-            const int mode = lds_fits ? (rects_fit ? 3 : (stack_fits ? 2 : 1)) : 0;
-            HIPC(c, launch_trace_wavepersist(dev_scene(c), job, c->d_samples, c->d_aux,
+            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits ? 2 : 1)) : 0;
+            DevScene sc = dev_scene(c);
+            if (c->opt_lds && c->opt_ww == 0 && (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
+                // nodes exceed the LDS budget (or an explicit cache size is set):
+                // cache the top of the breadth-first array
+                const size_t budget = c->opt_lds_split == 1 ? (size_t)(160 * 1024) * block / 2048
+                                                            : (size_t)c->opt_lds_split * 1024;
+                sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
+                mode = 4;
+            }
+            HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, mode, slots,
                                              block, c->opt_min_waves, c->opt_ww, c->stream));

@@ -167,6 +167,27 @@ template <typename N, typename R> __device__ __forceinline__ CompactView<N, R> v
     return CompactView<N, R>{n, r};
 }
 
+// Top-of-tree cache for scenes whose nodes exceed the LDS budget: production
+// float4s [0, n_lds) are staged in LDS, the rest are read from global memory.
+// Child pairs are numbered breadth-first at upload (mm_runtime.hip), so the
+// LDS part holds the top levels every traversal visits.
+struct SplitNodes {
+    const float4* lds;
+    const float4* glob;
+    uint32_t n_lds;
+};
+
+// The two children of an interior node: one adjacent 64-B pair at 2*lf.
+__device__ __forceinline__ void node_pair(const float4* n, uint32_t lf, float4& la, float4& lb, float4& ra,
+                                          float4& rb) {
+    la = n[2 * lf]; lb = n[2 * lf + 1]; ra = n[2 * lf + 2]; rb = n[2 * lf + 3];
+}
+__device__ __forceinline__ void node_pair(const SplitNodes& n, uint32_t lf, float4& la, float4& lb, float4& ra,
+                                          float4& rb) {
+    if (2 * lf < n.n_lds) node_pair(n.lds, lf, la, lb, ra, rb);
+    else node_pair(n.glob, lf, la, lb, ra, rb);
+}
+
 __device__ __forceinline__ float sel3(uint32_t a, F3 v) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
 
 // ray_rect_intersect on a compact record (FAST kind) for a fast-guarded ray;
@@ -232,7 +253,8 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, const V& v, const 
         return false;
     }
     if (kStats) c.visits++;
-    const float4 la = v.nodes[2 * lf], lb = v.nodes[2 * lf + 1], ra = v.nodes[2 * lf + 2], rb = v.nodes[2 * lf + 3];
+    float4 la, lb, ra, rb;
+    node_pair(v.nodes, lf, la, lb, ra, rb);
     float d1 = aabb_pairs<kFast>(la, lb, r, t);
     float d2 = aabb_pairs<kFast>(ra, rb, r, t);
     uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
@@ -279,8 +301,8 @@ __device__ __forceinline__ bool traverse_ww(const DevScene& sc, const V& v, cons
         while ((cur >> 24) == 0) {
             const uint32_t lf = cur & 0xFFFFFFu;
             if (kStats) c.visits++;
-            const float4 la = v.nodes[2 * lf], lb = v.nodes[2 * lf + 1], ra = v.nodes[2 * lf + 2],
-                         rb = v.nodes[2 * lf + 3];
+            float4 la, lb, ra, rb;
+            node_pair(v.nodes, lf, la, lb, ra, rb);
             const float d1 = aabb_pairs<kFast>(la, lb, r, t);
             const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
             const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
@@ -339,8 +361,8 @@ __device__ __forceinline__ bool traverse_lb(const DevScene& sc, const V& v, cons
         } else if (!done && !at_leaf) {
             const uint32_t lf = cur & 0xFFFFFFu;
             if (kStats) c.visits++;
-            const float4 la = v.nodes[2 * lf], lb = v.nodes[2 * lf + 1], ra = v.nodes[2 * lf + 2],
-                         rb = v.nodes[2 * lf + 3];
+            float4 la, lb, ra, rb;
+            node_pair(v.nodes, lf, la, lb, ra, rb);
             const float d1 = aabb_pairs<kFast>(la, lb, r, t);
             const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
             const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);

@@ -184,13 +184,22 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v,
 }
 
 // kLds: 0 nodes via L1/L2 + scratch stack, 1 nodes in LDS + scratch stack,
-// 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread).
+// 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread),
+// 3 nodes + compact rect records in LDS, 4 top of the tree in LDS (the first
+// sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2.
 template <bool kStats, int kLds, int kBlock, int kMinWaves, int kWW>
 __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
                                                                          float4* __restrict__ samples,
                                                                          unsigned long long* stats, uint32_t* err,
                                                                          uint32_t* work, uint32_t stack_slots) {
-    if constexpr (kLds > 0) {
+    if constexpr (kLds == 4) {
+        extern __shared__ float4 lds_top[];
+        for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds_top[i] = sc.nodes[i];
+        __syncthreads();
+        ScratchStack st;
+        wavepersist_body<kStats, kWW>(sc, view(SplitNodes{lds_top, sc.nodes, sc.n_lds_f4}), st, job, samples, stats,
+                                      err, work);
+    } else if constexpr (kLds > 0) {
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
         uint2* lds_recs = reinterpret_cast<uint2*>(lds_nodes + 2 * sc.n_nodes);
@@ -221,9 +230,10 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        uint32_t stack_slots, hipStream_t s) {
     const uint32_t block = kBlock;
-    const size_t lds = (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
-                       (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
-                       (kLds == 3 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
+    const size_t lds = kLds == 4 ? (size_t)sc.n_lds_f4 * sizeof(float4)
+                                 : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
+                                       (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
+                                       (kLds == 3 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves, kWW>
                             : k_trace_wavepersist<false, kLds, kBlock, kMinWaves, kWW>;
     int per_cu = 0, dev = 0, cus = 0;
@@ -250,7 +260,9 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
 #define MM_WP3(B, W, WW) \
     if (loop_form == WW) { MM_WP2(3, B, W, WW) MM_WP2(2, B, W, WW) MM_WP2(1, B, W, WW) MM_WP2(0, B, W, WW) }
 #define MM_WP(B, W) \
-    if (block == B && min_waves == W) { MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 8) MM_WP3(B, W, 16) MM_WP3(B, W, 32) }
+    if (block == B && min_waves == W) {                                                              \
+        if (loop_form == 0) { MM_WP2(4, B, W, 0) }                                                    \
+        MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 8) MM_WP3(B, W, 16) MM_WP3(B, W, 32) }
     MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
 #undef MM_WP
 #undef MM_WP3

@@ -40,6 +40,9 @@ for _b, _w in ((512, 6), (512, 8), (1024, 1), (1024, 8)):
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["ls"] = 0
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["lr"] = 0
     VARIANTS[f"wp-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1)
+for _kb in (0, 1, 16, 32, 48, 64, 80):
+    VARIANTS[f"wp-split{_kb}"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=_kb)
+    VARIANTS[f"wp-split{_kb}-b512-w6"] = dict(pipe=1, persist=2, lds=1, block=512, mw=6, split=_kb)
 for _b, _w in ((512, 6), (1024, 1), (1024, 8)):
     for _th in (0, 8, 16, 24, 32, 40, 48):
         VARIANTS[f"persist-lds-b{_b}-w{_w}-t{_th}"] = dict(pipe=1, persist=1, lds=1, block=_b, mw=_w, th=_th, lr=0)
@@ -83,6 +86,8 @@ def main():
             r.set_option(6, v["ls"])
         if "mw" in v:
             r.set_option(MM_OPT_MIN_WAVES, v["mw"])
+        if "split" in v:
+            r.set_option(9, v["split"])
         if "th" in v:
             r.set_option(MM_OPT_THRESHOLD, v["th"])
         out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")

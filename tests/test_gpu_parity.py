@@ -117,6 +117,8 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "leafbatch8-global": (1, {1: 0, 3: 2, 7: 8}),
     "whilewhile-global-ldsstack": (1, {1: 0, 3: 2, 7: 1, 6: 1}),
     "wavepersist-lds-b512-w8": (1, {1: 1, 3: 2, 2: 512, 5: 8}),
+    "wavepersist-split2kb": (1, {1: 1, 3: 2, 9: 2}),
+    "wavepersist-split20kb-b512-w6": (1, {1: 1, 3: 2, 9: 20, 2: 512, 5: 6}),
     "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
     "wavefront": (2, {}),
     "wavefront-global": (2, {1: 0}),
@@ -238,3 +240,29 @@ def test_argument_errors(ren, gpu):
     with pytest.raises(MMError) as ei:
         ren.upload_scene(bad)
     assert ei.value.code == -5  # MM_ERR_STACK
+
+
+@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}],
+                         ids=["auto-split", "split-off", "split-8kb", "global", "mega"])
+def test_large_scene_top_of_tree_cache(gpu, opts):
+    """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
+    default kernel caches the top of the breadth-first node array in LDS and
+    reads the rest through L1/L2.  Bit-exact vs the oracle at C5 limits."""
+    from mirror_maze import Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(64)
+    assert s.n_nodes * 32 > 160 * 1024
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload_scene(s)
+    u = default_uniform(3840, 2160, 0)
+    e = make_ext(4, 16, 16, frame=5)
+    for (x0, y0) in [(0, 0), (1900, 1000), (3000, 1800), (640, 1500)]:
+        got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
+        ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
+        assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
+        assert (st.rays, st.node_visits, st.rect_tests) == (rst.rays, rst.node_visits, rst.rect_tests)
+    r.close()
