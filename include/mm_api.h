@@ -10,6 +10,8 @@
  *       dispatch                src/main.rs:884-885  (32x24 groups of 32x32)
  *   - the Metal buffer plumbing  src/utils.rs:86-102 (make_buf/copy_to_buf)
  *   - device/queue creation      src/main.rs:616-626, 638-640
+ *   - the render pass's blur     src/main.rs:888-891, src/shaders.metal:214-225
+ *                                (mm_present)
  *
  * Conventions: 0 on success, a negative MM_ERR_* code otherwise (message via
  * mm_last_error); no exceptions or aborts cross the ABI; host memory is owned
@@ -74,6 +76,28 @@ int  mm_trace_chunks(mm_ctx* ctx, const mm_uniform* uni,
  * rgba8:    RGBA8Unorm as the texture stores it (round-to-nearest-even of
  *           clamp(x,0,1)*255), or NULL. */
 int  mm_read_framebuffer(mm_ctx* ctx, float* rgba_f32, uint8_t* rgba8);
+
+/* One presentation step: the render pass's fragment_shader 5-tap blur of the
+ * RGBA8 texture (src/main.rs:888-891, src/shaders.metal:214-225), as a Jacobi
+ * step — every texel reads the previous texture, neighbours outside it read 0,
+ * alpha is written as 1 — so the frame sequence is deterministic (the
+ * reference blurs in place from concurrent fragments).  Operation order of
+ * the compiled IR: c = (((L+R)+D)+U)*0.5 + C, then c * RN(1/3).  Acts on the
+ * RGBA8 texture only (the float framebuffer keeps the traced values). */
+int  mm_present(mm_ctx* ctx);
+
+/* The per-pixel packets of the last mm_trace_chunks, in the layout of the
+ * shaders.air revision's extra `device float4* pixel_data` output (the
+ * streaming-tile format): packets[(c*16 + pn)*4 ..] = (r, g, b,
+ * bitcast<float>(x << 16 | y)) for pixel pn = 0..15 of chunk c, x = chunk.x +
+ * pn/4, y = chunk.y + pn%4; rgb is the 64-sample mean before quantisation.
+ * packets: host buffer of n_chunks*16*4 floats; n_chunks <= the last dispatch's. */
+int  mm_read_packets(mm_ctx* ctx, float* packets, uint32_t n_chunks);
+
+/* Device-side RGBA8 quantisation of a float RGBA image (e.g. an mm_trace_tile
+ * output) with the texture-write conversion (round-to-nearest-even of
+ * clamp(x,0,1)*255, all four channels).  Queued on the context's stream. */
+int  mm_quantize_rgba8(mm_ctx* ctx, const float* rgba_dev, uint8_t* rgba8_dev, uint64_t n_pixels);
 
 /* ---- throughput mode: offline renderer ------------------------------------
  * Renders pixels (x0 + i, y0 + j*y_stride), 0<=i<w, 0<=j<h, of the frame

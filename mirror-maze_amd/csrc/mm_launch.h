@@ -88,6 +88,12 @@ hipError_t launch_wf_shade(const DevScene& sc, const TileJob& job, const WaveSta
                            float4* samples, unsigned long long* stats, uint32_t* err, bool count_stats,
                            hipStream_t s);
 
+// Display stage (display.hip).
+hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H, hipStream_t s);
+hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,
+                                float4* out, hipStream_t s);
+hipError_t launch_quantize(const float4* in, uint32_t* out, size_t n, hipStream_t s);
+
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);
 

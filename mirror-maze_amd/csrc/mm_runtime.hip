@@ -47,6 +47,10 @@ struct mm_ctx {
     // texout (parity mode)
     float4* d_fb = nullptr;
     uint32_t* d_fb8 = nullptr;
+    uint32_t* d_fb8_alt = nullptr;  // presentation blur target (swapped with d_fb8)
+    uint32_t last_chunks = 0;       // chunk count of the last mm_trace_chunks
+    float4* d_packets = nullptr;
+    size_t packets_cap = 0;
     uint32_t fb_w = 0, fb_h = 0;
     // chunk list (buffer 0)
     uint32_t* d_chunks = nullptr;
@@ -264,6 +268,7 @@ void mm_destroy(mm_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_scene(c);
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
+    (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -434,10 +439,12 @@ int mm_trace_chunks(mm_ctx* c, const mm_uniform* u, const uint32_t* chunks, uint
     const uint32_t W = (uint32_t)u->view_w, H = (uint32_t)u->view_h;
     HIPC(c, hipSetDevice(c->device));
     if (W != c->fb_w || H != c->fb_h) {
-        (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8);
-        c->d_fb = nullptr; c->d_fb8 = nullptr;
+        (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_fb8_alt);
+        c->d_fb = nullptr; c->d_fb8 = nullptr; c->d_fb8_alt = nullptr;
+        c->fb_w = c->fb_h = 0;
         HIPC(c, hipMalloc((void**)&c->d_fb, (size_t)W * H * sizeof(float4)));
         HIPC(c, hipMalloc((void**)&c->d_fb8, (size_t)W * H * sizeof(uint32_t)));
+        HIPC(c, hipMalloc((void**)&c->d_fb8_alt, (size_t)W * H * sizeof(uint32_t)));
         HIPC(c, hipMemsetAsync(c->d_fb, 0, (size_t)W * H * sizeof(float4), c->stream));
         HIPC(c, hipMemsetAsync(c->d_fb8, 0, (size_t)W * H * sizeof(uint32_t), c->stream));
         c->fb_w = W; c->fb_h = H;
@@ -451,7 +458,46 @@ int mm_trace_chunks(mm_ctx* c, const mm_uniform* u, const uint32_t* chunks, uint
     HIPC(c, launch_trace_chunks(dev_scene(c), *u, c->d_chunks, gw, gh, c->d_fb, c->d_fb8, c->d_aux,
                                 reinterpret_cast<uint32_t*>(c->d_aux + 4), false, c->stream));
     if ((rc = end_timing(c, 1))) return rc;
+    c->last_chunks = n_chunks;
     return read_aux(c, nullptr);
+}
+
+int mm_present(mm_ctx* c) {
+    if (!c) return MM_ERR_INVALID;
+    if (!c->d_fb8) return fail(c, MM_ERR_INVALID, "mm_present: nothing rendered yet");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, launch_present_blur(c->d_fb8, c->d_fb8_alt, c->fb_w, c->fb_h, c->stream));
+    std::swap(c->d_fb8, c->d_fb8_alt);
+    return MM_OK;
+}
+
+int mm_read_packets(mm_ctx* c, float* packets, uint32_t n_chunks) {
+    if (!c) return MM_ERR_INVALID;
+    if (!packets) return fail(c, MM_ERR_INVALID, "mm_read_packets: null output");
+    if (!c->d_fb || c->last_chunks == 0) return fail(c, MM_ERR_INVALID, "mm_read_packets: no mm_trace_chunks yet");
+    if (n_chunks > c->last_chunks)
+        return fail(c, MM_ERR_INVALID, "mm_read_packets: more chunks than the last dispatch used");
+    if (n_chunks == 0) return MM_OK;
+    HIPC(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->d_packets, c->packets_cap, 16 * (size_t)n_chunks);
+    if (rc) return rc;
+    HIPC(c, launch_chunk_packets(c->d_fb, c->d_chunks, n_chunks, c->fb_w, c->fb_h, c->d_packets, c->stream));
+    HIPC(c, hipMemcpyAsync(packets, c->d_packets, 16 * (size_t)n_chunks * sizeof(float4), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MM_OK;
+}
+
+int mm_quantize_rgba8(mm_ctx* c, const float* rgba_dev, uint8_t* rgba8_dev, uint64_t n_pixels) {
+    if (!c) return MM_ERR_INVALID;
+    if ((!rgba_dev || !rgba8_dev) && n_pixels) return fail(c, MM_ERR_INVALID, "mm_quantize_rgba8: null buffer");
+    if (n_pixels == 0) return MM_OK;
+    if (reinterpret_cast<uintptr_t>(rgba_dev) % 16 || reinterpret_cast<uintptr_t>(rgba8_dev) % 4)
+        return fail(c, MM_ERR_INVALID, "mm_quantize_rgba8: misaligned buffer");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, launch_quantize(reinterpret_cast<const float4*>(rgba_dev), reinterpret_cast<uint32_t*>(rgba8_dev),
+                            (size_t)n_pixels, c->stream));
+    return MM_OK;
 }
 
 int mm_read_framebuffer(mm_ctx* c, float* rgba, uint8_t* rgba8) {

@@ -91,6 +91,9 @@ EXPORTS = {
     "mm_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, P]),
     "mm_trace_chunks": (C.c_int, [P, C.POINTER(mm_uniform), P, C.c_uint32]),
     "mm_read_framebuffer": (C.c_int, [P, P, P]),
+    "mm_present": (C.c_int, [P]),
+    "mm_read_packets": (C.c_int, [P, P, C.c_uint32]),
+    "mm_quantize_rgba8": (C.c_int, [P, P, P, C.c_uint64]),
     "mm_trace_tile": (C.c_int, [P, C.POINTER(mm_uniform), C.POINTER(mm_ext), C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_uint32, C.c_uint32, P, C.POINTER(mm_stats)]),
     "mm_set_pipeline": (C.c_int, [P, C.c_int]),
@@ -118,6 +121,10 @@ EXPORTS = {
     "mm_chunks_total": (C.c_uint32, [P]),
     "mm_chunks_next": (C.c_int, [P, C.c_uint32, P]),
     "mm_chunks_free": (None, [P]),
+    # mm_io.h
+    "mm_write_ppm": (C.c_int, [C.c_char_p, P, C.c_uint32, C.c_uint32]),
+    "mm_write_png": (C.c_int, [C.c_char_p, P, C.c_uint32, C.c_uint32]),
+    "mm_quantize_rgba8_host": (None, [P, P, C.c_uint64]),
 }
 
 _lib = None

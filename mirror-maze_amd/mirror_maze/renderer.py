@@ -91,6 +91,31 @@ class Renderer:
         self._check(lib().mm_read_framebuffer(self._ctx, f.ctypes.data, b.ctypes.data))
         return f, b
 
+    def present(self) -> None:
+        """One presentation step: the fragment_shader blur of the RGBA8 texture
+        as a Jacobi step (src/shaders.metal:214-225; mm_present)."""
+        self._check(lib().mm_present(self._ctx))
+
+    def read_packets(self, n_chunks: int) -> np.ndarray:
+        """(n_chunks, 16, 4) float32 packets of the last compute_shader: rgb and
+        bitcast(x << 16 | y) (the shaders.air revision's pixel_data output)."""
+        out = np.zeros((n_chunks, 16, 4), dtype=np.float32)
+        self._check(lib().mm_read_packets(self._ctx, out.ctypes.data, n_chunks))
+        return out
+
+    def quantize(self, rgba):
+        """RGBA8 (uint8 CUDA tensor, same shape) of a float32 RGBA CUDA tensor,
+        with the texture-write conversion (mm_quantize_rgba8)."""
+        import torch
+
+        if not (rgba.is_cuda and rgba.dtype == torch.float32 and rgba.is_contiguous() and rgba.shape[-1] == 4):
+            raise ValueError("rgba must be a contiguous float32 CUDA tensor [..., 4]")
+        out = torch.empty(rgba.shape, dtype=torch.uint8, device=rgba.device)
+        if not self._pinned_stream:
+            self._check(lib().mm_set_stream(self._ctx, torch.cuda.current_stream(rgba.device).cuda_stream))
+        self._check(lib().mm_quantize_rgba8(self._ctx, rgba.data_ptr(), out.data_ptr(), rgba.numel() // 4))
+        return out
+
     # -- throughput mode ------------------------------------------------------
     def trace_tile(self, uniform: _lib.mm_uniform, ext: _lib.mm_ext, x0: int, y0: int, w: int, h: int,
                    y_stride: int = 1, out=None, stats: bool = False):

@@ -406,3 +406,40 @@ int oracle_trace_tile(const oracle_scene* sc, const mm_uniform* u, const mm_ext*
     add_stats(st, rays, &tr, (uint64_t)w * h * e->spp);
     return MM_OK;
 }
+
+/* ---- display stage (TEST INFRASTRUCTURE) -------------------------------------
+ * fragment_shader (src/shaders.metal:214-225) as a Jacobi step, in the
+ * operation order of the compiled IR (src/shaders.ir, fragment_shader):
+ *   s = ((L + R) + D) + U;  s = s * 0.5;  s = s + C;  s = s * RN(1/3)
+ * texel reads c/255 (IEEE division), neighbours outside the texture read 0,
+ * the write quantises with round-half-even of clamp(x,0,1)*255, alpha 255. */
+static inline uint8_t q8(float x) {
+    x = fminf(fmaxf(x, 0.0f), 1.0f);
+    return (uint8_t)nearbyintf(x * 255.0f);
+}
+
+static inline v3 tex_rd(const uint8_t* t, int x, int y, int W, int H) {
+    if (x < 0 || y < 0 || x >= W || y >= H) return mk(0.0f, 0.0f, 0.0f);
+    const uint8_t* p = t + 4 * ((size_t)y * W + x);
+    return mk((float)p[0] / 255.0f, (float)p[1] / 255.0f, (float)p[2] / 255.0f);
+}
+
+void oracle_present_blur(const uint8_t* in, uint8_t* out, uint32_t W, uint32_t H) {
+    const float third = 0x1.555556p-2f;
+    for (int y = 0; y < (int)H; ++y)
+        for (int x = 0; x < (int)W; ++x) {
+            const v3 c = tex_rd(in, x, y, W, H);
+            const v3 r = tex_rd(in, x + 1, y, W, H), l = tex_rd(in, x - 1, y, W, H);
+            const v3 d = tex_rd(in, x, y + 1, W, H), u = tex_rd(in, x, y - 1, W, H);
+            v3 s = vadd(vadd(vadd(l, r), d), u);
+            s = mk(s.x * 0.5f, s.y * 0.5f, s.z * 0.5f);
+            s = vadd(s, c);
+            s = mk(s.x * third, s.y * third, s.z * third);
+            uint8_t* o = out + 4 * ((size_t)y * W + x);
+            o[0] = q8(s.x); o[1] = q8(s.y); o[2] = q8(s.z); o[3] = 255;
+        }
+}
+
+void oracle_quantize(const float* rgba, uint8_t* rgba8, uint64_t n_pixels) {
+    for (uint64_t i = 0; i < 4 * n_pixels; ++i) rgba8[i] = q8(rgba[i]);
+}

@@ -58,6 +58,11 @@ int oracle_trace_path(const oracle_scene* sc, const float ori[3], const float di
                       uint32_t seed, int bounce_limit, int mirror_limit,
                       float rgb_out[3], uint32_t* rays);
 
+/* Display stage: fragment_shader blur as a Jacobi step (RGBA8 in -> out,
+ * W x H, in != out) and the RGBA8 store conversion. */
+void oracle_present_blur(const uint8_t* in, uint8_t* out, uint32_t W, uint32_t H);
+void oracle_quantize(const float* rgba, uint8_t* rgba8, uint64_t n_pixels);
+
 /* Pieces exported for unit tests. */
 float    oracle_rand_pm1(uint32_t* state);          /* (random(state)-0.5)*2 */
 uint32_t oracle_seed_reference(uint32_t tx, uint32_t ty, uint32_t time);

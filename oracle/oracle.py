@@ -57,6 +57,10 @@ def lib():
         L.oracle_primary_dir.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.oracle_intersect_aabb.argtypes = [P, P, C.c_float, P, P]
         L.oracle_intersect_aabb.restype = C.c_float
+        L.oracle_present_blur.argtypes = [P, P, C.c_uint32, C.c_uint32]
+        L.oracle_present_blur.restype = None
+        L.oracle_quantize.argtypes = [P, P, C.c_uint64]
+        L.oracle_quantize.restype = None
         _lib = L
     return _lib
 
@@ -124,3 +128,38 @@ class Oracle:
         rc = lib().oracle_trace_path(C.byref(self.sc), o.ctypes.data, dd.ctypes.data, seed, bounce_limit,
                                      mirror_limit, rgb.ctypes.data, C.byref(rays))
         return rgb, rays.value, rc
+
+
+def present_blur(tex: np.ndarray) -> np.ndarray:
+    """One Jacobi blur step of an (H, W, 4) uint8 texture (oracle_present_blur)."""
+    tex = np.ascontiguousarray(tex, dtype=np.uint8)
+    out = np.empty_like(tex)
+    lib().oracle_present_blur(tex.ctypes.data, out.ctypes.data, tex.shape[1], tex.shape[0])
+    return out
+
+
+def quantize(rgba: np.ndarray) -> np.ndarray:
+    rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+    out = np.empty(rgba.shape, dtype=np.uint8)
+    lib().oracle_quantize(rgba.ctypes.data, out.ctypes.data, rgba.size // 4)
+    return out
+
+
+class DisplayLoop:
+    """The reference's per-frame sequence on the RGBA8 screen texture
+    (src/main.rs:860-894): compute_shader writes the traced chunks' texels,
+    then the fragment_shader blur runs over the whole texture."""
+
+    def __init__(self, oracle: Oracle, W: int, H: int):
+        self.o = oracle
+        self.tex = np.zeros((H, W, 4), dtype=np.uint8)
+
+    def frame(self, uniform, chunks, present: bool = True) -> np.ndarray:
+        H, W = self.tex.shape[:2]
+        fb = np.full((H, W, 4), np.nan, dtype=np.float32)
+        self.o.trace_chunks(uniform, chunks, fb=fb)
+        written = ~np.isnan(fb[..., 0])
+        self.tex[written] = quantize(fb[written])
+        if present:
+            self.tex = present_blur(self.tex)
+        return self.tex
