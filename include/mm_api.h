@@ -128,12 +128,17 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_THRESHOLD   4   /* persistent kernel: traverse while > N lanes traverse (0..63) */
 #define MM_OPT_MIN_WAVES   5   /* wave-persistent kernel register budget: 1, 6 or 8 (default) waves/SIMD */
 #define MM_OPT_TRAVERSAL   7   /* wave-persistent kernel loop form: 0 if-if (default), 1 while-while,
+                                  2 lean if-if (one pop site, no overflow test),
+                                  3 if-if with the stack top in a register,
+                                  4 if-if, lanes refilled with new paths at every bounce,
                                   8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
 #define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
 #define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 0 scratch (default) */
 #define MM_OPT_LDS_SPLIT   9   /* wave-persistent kernel, BVH larger than the LDS budget: cache the top of
                                   the (breadth-first) node array in LDS, rest via L1/L2.
                                   0 off, 1 auto size (default), >1: always use a cache of this many KB */
+#define MM_OPT_COLD_LDS   10   /* wave-persistent kernel: 1 park each path's T and L in LDS while its ray
+                                  traverses (frees registers; nodes in LDS, no rect records), 0 off (default) */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Wait for all work queued by this context. */

@@ -69,6 +69,7 @@ struct mm_ctx {
     int pipe = MM_PIPE_AUTO;
     bool opt_lds = true;
     uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto size, else KB
+    bool opt_cold_lds = false;      // park T and L in LDS during traversal
     uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
     // Megakernel form (measured on C3, profiles/r01_ab_*.txt): wave-persistent
     // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
@@ -306,11 +307,13 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_LDS_STACK: c->opt_lds_stack = value != 0; return MM_OK;
         case MM_OPT_TRAVERSAL:
-            if (value != 0 && value != 1 && value != 8 && value != 16 && value != 32)
-                return fail(c, MM_ERR_INVALID, "traversal loop form must be 0, 1, 8, 16 or 32");
+            if (value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 8 && value != 16 &&
+                value != 32)
+                return fail(c, MM_ERR_INVALID, "traversal loop form must be 0, 1, 2, 3, 4, 8, 16 or 32");
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
+        case MM_OPT_COLD_LDS: c->opt_cold_lds = value != 0; return MM_OK;
         case MM_OPT_LDS_SPLIT:
             if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
             c->opt_lds_split = (uint32_t)value;
@@ -580,9 +583,13 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= (size_t)(160 * 1024) * block / 2048;
             const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
             const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * block / 2048;
-            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits ? 2 : 1)) : 0;
+            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && c->opt_ww != 4 ? 2 : 1)) : 0;
+            const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
+            if (lds_fits && c->opt_cold_lds && c->opt_ww == 0 && lds_cold <= (size_t)(160 * 1024) * block / 2048)
+                mode = 5;
             DevScene sc = dev_scene(c);
-            if (c->opt_lds && c->opt_ww == 0 && (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
+            if (c->opt_lds && (c->opt_ww == 0 || c->opt_ww == 2 || c->opt_ww == 3 || c->opt_ww == 4) &&
+                (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
                 // nodes exceed the LDS budget (or an explicit cache size is set):
                 // cache the top of the breadth-first array
                 const size_t budget = c->opt_lds_split == 1 ? (size_t)(160 * 1024) * block / 2048

@@ -130,6 +130,22 @@ struct ScratchStack {          // the reference's 50-entry private array
     __device__ __forceinline__ void push(uint32_t i, uint32_t v) { s[i] = v; }
     __device__ __forceinline__ uint32_t pop(uint32_t i) const { return s[i]; }
 };
+// The same stack with its top entry held in a register: a pop returns the
+// register and reloads the next entry from scratch, whose latency then
+// overlaps the following traversal step instead of stalling the next node
+// fetch.  mem[k] holds entry k-1 (mem[0] is a dummy), so push and pop are
+// unconditional.
+struct RegTopStack {
+    uint32_t top = 0;
+    uint32_t mem[kStackMax + 1];
+    static constexpr uint32_t kCap = kStackMax;
+    __device__ __forceinline__ void push(uint32_t i, uint32_t v) { mem[i] = top; top = v; }
+    __device__ __forceinline__ uint32_t pop(uint32_t i) {
+        const uint32_t r = top;
+        top = mem[i];
+        return r;
+    }
+};
 // u16 entries in LDS, [slot][thread] so a wave's same-slot accesses are
 // contiguous: (count << 12 | left_first) needs count < 16, left_first < 4096
 // and slots >= tree depth -- all checked at upload.
@@ -285,6 +301,44 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, const V& v, const R
     return !ovf;
 }
 
+// Lean form (MM_OPT_TRAVERSAL 2): the same iteration with one pop site and no
+// overflow test.  mm_upload_scene rejects trees deeper than the stack (50
+// entries, or the LDS stack's depth-sized slots), and near-first traversal
+// holds at most one pending far child per level of the current root-to-node
+// path, so a push can never overflow.  Per lane the visits, pushes and pops
+// are exactly trav_step's.
+template <bool kFast, bool kStats, typename V, typename Stack>
+__device__ __forceinline__ bool traverse_lean(const DevScene& sc, const V& v, const Ray& r, float& t,
+                                              uint32_t& index, Stack& stack, Counters& c) {
+    uint32_t cur = sc.root_packed, head = 0;
+    for (;;) {
+        const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+        bool pop;
+        if (cnt > 0) {
+            leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
+            if (kStats) c.rtests += cnt;
+            pop = true;
+        } else {
+            if (kStats) c.visits++;
+            float4 la, lb, ra, rb;
+            node_pair(v.nodes, lf, la, lb, ra, rb);
+            const float d1 = aabb_pairs<kFast>(la, lb, r, t);
+            const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
+            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+            const bool sw = d1 > d2;
+            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
+            cur = sw ? pr : pl;
+            pop = dn == kBig;
+            if (!pop && df != kBig) stack.push(head++, sw ? pl : pr);
+        }
+        if (pop) {
+            if (head == 0) break;
+            cur = stack.pop(--head);
+        }
+    }
+    return true;
+}
+
 // "while-while" form of the same traversal: each lane runs interior steps
 // until it reaches a leaf (or finishes), then the wave's leaves are processed
 // together.  Per lane the sequence of node visits, rect tests, pushes and
@@ -429,7 +483,10 @@ template <bool kStats, typename V, typename Stack, int kWW = 0>
 __device__ __forceinline__ bool closest_hit(const DevScene& sc, const V& v, F3 o, F3 d, float& t,
                                             uint32_t& index, Stack& stack, Counters& c) {
     const Ray r = make_ray(o, d);
-    if constexpr (kWW >= 2) {
+    if constexpr (kWW == 2) {
+        if (sc.fast_ok && ray_fast_ok(r)) return traverse_lean<true, kStats>(sc, v, r, t, index, stack, c);
+        return traverse_lean<false, kStats>(sc, v, r, t, index, stack, c);
+    } else if constexpr (kWW >= 8) {
         if (sc.fast_ok && ray_fast_ok(r)) return traverse_lb<true, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
         return traverse_lb<false, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
     } else if constexpr (kWW == 1) {
@@ -487,12 +544,32 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
     return true;
 }
 
+// Where a path's throughput T and radiance L live while its ray traverses
+// (they are only touched by shading): in registers (NoCold), or parked in LDS,
+// [field][thread], which frees six VGPRs for the traversal loop.
+struct NoCold {
+    __device__ __forceinline__ void save(const F3&, const F3&) const {}
+    __device__ __forceinline__ void restore(F3&, F3&) const {}
+};
+struct LdsCold {
+    float* base;        // &lds[field 0][this thread]
+    uint32_t stride;    // threads per block
+    __device__ __forceinline__ void save(const F3& T, const F3& L) const {
+        base[0] = T.x; base[stride] = T.y; base[2 * stride] = T.z;
+        base[3 * stride] = L.x; base[4 * stride] = L.y; base[5 * stride] = L.z;
+    }
+    __device__ __forceinline__ void restore(F3& T, F3& L) const {
+        T = F3{base[0], base[stride], base[2 * stride]};
+        L = F3{base[3 * stride], base[4 * stride], base[5 * stride]};
+    }
+};
+
 // Whole path (shaders.metal:302-344): returns sqrt(max(L, 0)).
 // kRef selects traverse_reference (MM_PIPE_REFERENCE).
-template <bool kStats, bool kRef, typename V, typename Stack, int kWW = 0>
+template <bool kStats, bool kRef, typename V, typename Stack, int kWW = 0, typename Cold = NoCold>
 __device__ __forceinline__ F3 trace_path(const DevScene& sc, const V& v, F3 ori, F3 dir, uint32_t seed,
                                          int bounce_limit, int mirror_limit, Stack& stack, Counters& c,
-                                         bool& overflow) {
+                                         bool& overflow, const Cold& cold = Cold{}) {
     PathState p;
     p.ori = ori; p.dir = dir; p.seed = seed;
     p.T = F3{1.0f, 1.0f, 1.0f};
@@ -502,8 +579,10 @@ __device__ __forceinline__ F3 trace_path(const DevScene& sc, const V& v, F3 ori,
         float t = kBig;
         uint32_t k = 0;
         bool ok;
+        cold.save(p.T, p.L);
         if constexpr (kRef) ok = traverse_reference<kStats>(sc, make_ray(p.ori, p.dir), t, k, stack, c);
         else ok = closest_hit<kStats, V, Stack, kWW>(sc, v, p.ori, p.dir, t, k, stack, c);
+        cold.restore(p.T, p.L);
         if (kStats) c.rays++;
         if (!ok) { overflow = true; break; }
         if (!shade_step(sc, p, t, k, mirror_limit)) break;

@@ -6,6 +6,8 @@
 //   k_resolve         per-pixel sample reduction in the reference's order
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "mm_launch.h"
 #include "mm_trace.h"
 
@@ -150,10 +152,11 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // each wave takes 64 consecutive paths at a time from a global counter and
 // traces them exactly like k_trace_mega, so no block waits for its slowest
 // wave before the CU can take more work.
-template <bool kStats, int kWW, typename V, typename Stack>
+template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
 __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v, Stack& stack,
                                                  const TileJob& job, float4* __restrict__ samples,
-                                                 unsigned long long* stats, uint32_t* err, uint32_t* work) {
+                                                 unsigned long long* stats, uint32_t* err, uint32_t* work,
+                                                 const Cold& cold = Cold{}) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;
     const uint32_t lane = threadIdx.x & 63u;
@@ -174,7 +177,7 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v,
             const F3 d = jitter(primary_dir(job.u, px, py), seed);
             bool overflow = false;
             const F3 s = trace_path<kStats, false, V, Stack, kWW>(sc, v, ori, d, seed, (int)job.e.bounce_limit,
-                                                                  (int)job.e.mirror_limit, stack, c, overflow);
+                                                                  (int)job.e.mirror_limit, stack, c, overflow, cold);
             if (overflow) atomicOr(err, 1u);
             samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
@@ -183,10 +186,107 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v,
     if (kStats) flush_stats(stats, c, paths);
 }
 
+// Bounce-refill form of the wave-persistent body (loop form 4): a lane whose
+// path ends takes the next path of the wave's chunk at the next bounce
+// boundary instead of idling until the wave's longest path ends.  The wave
+// runs one bounce (closest hit + shade) per iteration for all lanes; every
+// path's operation sequence is trace_path's, so samples are bit-identical.
+template <bool kStats, typename V, typename Stack, typename Cold = NoCold>
+__device__ __forceinline__ void bouncerefill_body(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
+                                                  float4* __restrict__ samples, unsigned long long* stats,
+                                                  uint32_t* err, uint32_t* work) {
+    const uint32_t spp = job.e.spp;
+    const uint32_t n_paths = job.w * job.h * spp;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int bounce_limit = (int)job.e.bounce_limit, mirror_limit = (int)job.e.mirror_limit;
+    Counters c;
+    uint32_t paths = 0;
+    uint32_t chunk_base = 0, chunk_end = 0;  // wave-uniform
+    bool more = true, active = false;
+    uint32_t pid = 0;
+    PathState p;
+    for (;;) {
+        const uint64_t idle = __ballot(!active);
+        if (idle && (more || chunk_base < chunk_end)) {
+            const uint32_t need = (uint32_t)__popcll(idle), rank = (uint32_t)__popcll(idle & lt);
+            const uint32_t take1 = min(need, chunk_end - chunk_base);
+            bool got = !active && rank < take1;
+            uint32_t mine = chunk_base + rank;
+            chunk_base += take1;
+            if (take1 < need && more) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(work, 64u);
+                b = __shfl(b, 0);
+                if (b >= n_paths) {
+                    more = false;
+                } else {
+                    chunk_base = b;
+                    chunk_end = min(b + 64u, n_paths);
+                    const uint32_t take2 = min(need - take1, chunk_end - chunk_base);
+                    if (!active && rank >= take1 && rank < take1 + take2) {
+                        got = true;
+                        mine = chunk_base + (rank - take1);
+                    }
+                    chunk_base += take2;
+                }
+            }
+            if (got) {
+                pid = mine;
+                const uint32_t pix = mine / spp, smp = mine - pix * spp;
+                const uint32_t j = pix / job.w, i = pix - j * job.w;
+                const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
+                p.seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
+                p.dir = jitter(primary_dir(job.u, px, py), p.seed);
+                p.ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
+                p.T = F3{1.0f, 1.0f, 1.0f};
+                p.L = F3{0.0f, 0.0f, 0.0f};
+                p.n = 0;
+                p.mh = 0;
+                active = true;
+            }
+        }
+        if (!__ballot(active)) break;
+        if (active) {
+            bool fin = !(p.n < bounce_limit + p.mh);
+            if (!fin) {  // one bounce: shaders.metal:306-340
+                float t = kBig;
+                uint32_t k = 0;
+                const bool ok = closest_hit<kStats, V, Stack, 0>(sc, v, p.ori, p.dir, t, k, stack, c);
+                if (kStats) c.rays++;
+                if (!ok) atomicOr(err, 1u);
+                fin = !ok || !shade_step(sc, p, t, k, mirror_limit);
+                p.n++;
+                fin = fin || !(p.n < bounce_limit + p.mh);
+            }
+            if (fin) {
+                samples[pid] = make_float4(sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)),
+                                           sqrtf(fmaxf(p.L.z, 0.0f)), 0.0f);
+                paths++;
+                active = false;
+            }
+        }
+    }
+    if (kStats) flush_stats(stats, c, paths);
+}
+
+template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
+__device__ __forceinline__ void wp_dispatch(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
+                                            float4* __restrict__ samples, unsigned long long* stats, uint32_t* err,
+                                            uint32_t* work, const Cold& cold = Cold{}) {
+    if constexpr (kWW == 4) bouncerefill_body<kStats>(sc, v, stack, job, samples, stats, err, work);
+    else wavepersist_body<kStats, kWW>(sc, v, stack, job, samples, stats, err, work, cold);
+}
+
+// Traversal stack of the wave-persistent kernel: loop form 3 is the if-if loop
+// with the register-top stack (RegTopStack), every other form the scratch array.
+template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, ScratchStack>;
+
 // kLds: 0 nodes via L1/L2 + scratch stack, 1 nodes in LDS + scratch stack,
 // 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread),
 // 3 nodes + compact rect records in LDS, 4 top of the tree in LDS (the first
-// sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2.
+// sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2,
+// 5 nodes in LDS + each path's T and L parked in LDS while it traverses.
 template <bool kStats, int kLds, int kBlock, int kMinWaves, int kWW>
 __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
                                                                          float4* __restrict__ samples,
@@ -196,8 +296,8 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
         extern __shared__ float4 lds_top[];
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds_top[i] = sc.nodes[i];
         __syncthreads();
-        ScratchStack st;
-        wavepersist_body<kStats, kWW>(sc, view(SplitNodes{lds_top, sc.nodes, sc.n_lds_f4}), st, job, samples, stats,
+        WpStack<kWW> st;
+        wp_dispatch<kStats, kWW>(sc, view(SplitNodes{lds_top, sc.nodes, sc.n_lds_f4}), st, job, samples, stats,
                                       err, work);
     } else if constexpr (kLds > 0) {
         extern __shared__ float4 lds_nodes[];
@@ -207,21 +307,25 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
             for (uint32_t i = threadIdx.x; i < 5 * sc.n_rects; i += blockDim.x) lds_recs[i] = sc.recs[i];
         __syncthreads();
         if constexpr (kLds == 3) {
-            ScratchStack st;
-            wavepersist_body<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
+            WpStack<kWW> st;
+            wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
+        } else if constexpr (kLds == 5) {
+            WpStack<kWW> st;
+            const LdsCold cold{reinterpret_cast<float*>(lds_recs) + threadIdx.x, blockDim.x};
+            wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work, cold);
         } else if constexpr (kLds == 2) {
             LdsStack16 st;
             st.base = reinterpret_cast<uint16_t*>(lds_recs) + threadIdx.x;
             st.stride = blockDim.x;
             st.cap = stack_slots;
-            wavepersist_body<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         } else {
-            ScratchStack st;
-            wavepersist_body<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            WpStack<kWW> st;
+            wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         }
     } else {
-        ScratchStack st;
-        wavepersist_body<kStats, kWW>(sc, view(sc.nodes), st, job, samples, stats, err, work);
+        WpStack<kWW> st;
+        wp_dispatch<kStats, kWW>(sc, view(sc.nodes), st, job, samples, stats, err, work);
     }
 }
 
@@ -232,6 +336,7 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     const uint32_t block = kBlock;
     const size_t lds = kLds == 4 ? (size_t)sc.n_lds_f4 * sizeof(float4)
                                  : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
+                                       (kLds == 5 ? 6 * (size_t)block * sizeof(float) : 0) +
                                        (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
                                        (kLds == 3 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves, kWW>
@@ -262,7 +367,12 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
 #define MM_WP(B, W) \
     if (block == B && min_waves == W) {                                                              \
         if (loop_form == 0) { MM_WP2(4, B, W, 0) }                                                    \
-        MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 8) MM_WP3(B, W, 16) MM_WP3(B, W, 32) }
+        if (loop_form == 2) { MM_WP2(4, B, W, 2) }                                                    \
+        if (loop_form == 3) { MM_WP2(4, B, W, 3) }                                                    \
+        if (loop_form == 0) { MM_WP2(5, B, W, 0) }                                                    \
+        if (loop_form == 4) { MM_WP2(4, B, W, 4) MM_WP2(3, B, W, 4) MM_WP2(1, B, W, 4) MM_WP2(0, B, W, 4) }  \
+        MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 2) MM_WP3(B, W, 3) MM_WP3(B, W, 8) MM_WP3(B, W, 16)  \
+        MM_WP3(B, W, 32) }
     MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
 #undef MM_WP
 #undef MM_WP3

@@ -40,6 +40,21 @@ for _b, _w in ((512, 6), (512, 8), (1024, 1), (1024, 8)):
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["ls"] = 0
     VARIANTS[f"wp-lds-b{_b}-w{_w}"]["lr"] = 0
     VARIANTS[f"wp-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1)
+for _b, _w in ((512, 6), (1024, 8), (1024, 1)):
+    VARIANTS[f"lean-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1, ww=2)
+    VARIANTS[f"lean-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=0, ww=2)
+    VARIANTS[f"lean-ldsstack-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=1, lr=0, ww=2)
+    VARIANTS[f"lean-split1-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, split=1, ww=2)
+for _b, _w in ((512, 6), (1024, 8), (1024, 1)):
+    VARIANTS[f"rt-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1, ww=3)
+    VARIANTS[f"rt-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=0, ww=3)
+for _b, _w in ((512, 6), (512, 8), (1024, 8), (1024, 1)):
+    VARIANTS[f"cold-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=0, cold=1)
+for _b, _w in ((512, 6), (1024, 8), (1024, 1)):
+    VARIANTS[f"br-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1, ww=4)
+    VARIANTS[f"br-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=0, ww=4)
+VARIANTS["br-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=4)
+VARIANTS["rt-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=3)
 for _kb in (0, 1, 16, 32, 48, 64, 80):
     VARIANTS[f"wp-split{_kb}"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=_kb)
     VARIANTS[f"wp-split{_kb}-b512-w6"] = dict(pipe=1, persist=2, lds=1, block=512, mw=6, split=_kb)
@@ -86,6 +101,8 @@ def main():
             r.set_option(6, v["ls"])
         if "mw" in v:
             r.set_option(MM_OPT_MIN_WAVES, v["mw"])
+        if "cold" in v:
+            r.set_option(10, v["cold"])
         if "split" in v:
             r.set_option(9, v["split"])
         if "th" in v:

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc passes (scripts/pmc.sh output) for one kernel.
 
-    python scripts/pmc_summary.py gpurun_out/<tag> [kernel-substring] > profiles/<name>.txt
+    python scripts/pmc_summary.py gpurun_out/<tag> [kernel-substring [traffic.json]] > profiles/<name>.txt
 Per-dispatch means of every counter, plus derived metrics:
   lane utilisation = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
   VALU issue share = SQ_INSTS_VALU / (SIMDs * cycles / 2)   (wave64 VALU = 2 cycles on SIMD32)
@@ -37,3 +37,11 @@ if "FETCH_SIZE" in m:
     print(f"HBM fetch bytes (x2 corr.)   {2 * m['FETCH_SIZE'] * 1024:.6g}")
 if "WRITE_SIZE" in m:
     print(f"HBM write bytes              {m['WRITE_SIZE'] * 1024:.6g}")
+if len(sys.argv) > 3 and "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+    # bench.py reads this as roofline.traffic (HBM bytes per launch of the dominant kernel)
+    import json
+    rec = {"kernel_pattern": pat, "source": root.name,
+           "fetch_bytes_corrected": 2 * m["FETCH_SIZE"] * 1024, "write_bytes": m["WRITE_SIZE"] * 1024,
+           "hbm_bytes_per_launch": 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024,
+           "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, per-dispatch mean"}
+    Path(sys.argv[3]).write_text(json.dumps(rec, indent=1) + "\n")

@@ -118,6 +118,17 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "whilewhile-global-ldsstack": (1, {1: 0, 3: 2, 7: 1, 6: 1}),
     "wavepersist-lds-b512-w8": (1, {1: 1, 3: 2, 2: 512, 5: 8}),
     "wavepersist-split2kb": (1, {1: 1, 3: 2, 9: 2}),
+    "lean-ldsrects": (1, {1: 1, 3: 2, 7: 2, 8: 1}),
+    "lean-ldsstack": (1, {1: 1, 3: 2, 7: 2, 6: 1, 8: 0}),
+    "lean-global-b512-w6": (1, {1: 0, 3: 2, 7: 2, 2: 512, 5: 6}),
+    "lean-split2kb": (1, {1: 1, 3: 2, 7: 2, 9: 2}),
+    "regtop-ldsrects": (1, {1: 1, 3: 2, 7: 3, 8: 1}),
+    "coldlds": (1, {1: 1, 3: 2, 10: 1}),
+    "bouncerefill-ldsrects": (1, {1: 1, 3: 2, 7: 4, 8: 1}),
+    "bouncerefill-global-b512-w6": (1, {1: 0, 3: 2, 7: 4, 2: 512, 5: 6}),
+    "bouncerefill-split2kb": (1, {1: 1, 3: 2, 7: 4, 9: 2}),
+    "coldlds-b512-w6": (1, {1: 1, 3: 2, 10: 1, 2: 512, 5: 6}),
+    "regtop-split2kb-b512-w6": (1, {1: 1, 3: 2, 7: 3, 9: 2, 2: 512, 5: 6}),
     "wavepersist-split20kb-b512-w6": (1, {1: 1, 3: 2, 9: 20, 2: 512, 5: 6}),
     "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
     "wavefront": (2, {}),
@@ -156,7 +167,8 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
     ren.close()
 
 
-@pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects"])
+@pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
+                                  "lean-ldsrects", "bouncerefill-ldsrects"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
