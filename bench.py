@@ -9,7 +9,8 @@ query (src/shaders.metal:307).
 
 N GPUs (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 the frame's rows are interleaved over ranks (rank r renders rows r, r+N, ...),
-and rank 0 receives every tile with one RCCL gather per frame (north star:
+and rank 0 receives every tile with one RCCL gather per frame, overlapped with
+the next frame's trace (north star:
 "tiles of the framebuffer shard one-per-GPU ... single RCCL gather at frame
 end").  Total work is fixed as N grows -> "scaling": "strong".
 
@@ -124,23 +125,32 @@ def main():
     u = default_uniform(W, H, 0)
 
     # rows r, r+world, ... (mirror_maze/dist.py); pad so every rank sends the same shape
-    from mirror_maze.dist import gather_frame, row_shard, rows_max
+    from mirror_maze.dist import FrameGatherer, row_shard, rows_max
 
     y0, y_stride, my_rows = row_shard(H, world, rank)
-    tile = torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev)
     frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    # one RCCL gather per frame, issued async and double-buffered so it overlaps
+    # the next frame's trace (mirror_maze/dist.py: FrameGatherer)
+    gatherer = FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf) if world > 1 else None
+    tile1 = torch.zeros((H, W, 4), dtype=torch.float32, device=dev) if world == 1 else None
 
     def step(frame, stats=False):
         ext = make_ext(spp, bl, ml, frame=frame)
+        tile = gatherer.tile() if gatherer else tile1
         _, st = ren.trace_tile(u, ext, 0, y0, W, my_rows, y_stride=y_stride, out=tile[:my_rows], stats=stats)
-        if world > 1:
-            gather_frame(tile, H, dst=0, out=frame_buf)  # one RCCL gather per frame
+        if gatherer:
+            gatherer.put()
         else:
             frame_buf.copy_(tile[:H])
         return st
 
+    def drain():
+        if gatherer:
+            gatherer.flush()
+
     for i in range(args.warmup):
         step(10_000 + i)
+    drain()
     ren.set_profiling(True)
     ren.kernel_timing(reset=True)
     if world > 1:
@@ -149,6 +159,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    drain()  # the last frame's gather + assembly is inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -161,6 +172,7 @@ def main():
     for i in range(args.steps):
         st = step(i, stats=True)
         rays += st.rays; paths += st.paths; visits += st.node_visits; rtests += st.rect_tests
+    drain()
     counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
     t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:

@@ -48,6 +48,61 @@ def _worker(rank, world, port, H, W, q):
     dist.destroy_process_group()
 
 
+def _worker_pipelined(rank, world, port, H, W, q):
+    """Three frames through FrameGatherer (async, double-buffered gathers)."""
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo))
+    sys.path.insert(0, str(repo / "mirror-maze_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mirror_maze import Scene, default_uniform, make_ext
+    from mirror_maze.dist import FrameGatherer, row_shard, rows_max
+    from oracle.oracle import Oracle
+
+    s = Scene.build(10, 0)
+    o = Oracle.from_scene(s)
+    u = default_uniform(W, H, 0)
+    y0, stride, rows = row_shard(H, world, rank)
+    g = FrameGatherer((rows_max(H, world), W, 4), H, "cpu")
+    frames = []
+    for f in range(3):
+        t = g.tile().numpy()
+        o.trace_tile(u, make_ext(2, 3, 15, frame=f), 0, y0, W, rows, y_stride=stride, out=t[:rows])
+        g.put()
+        if rank == 0 and f >= 1:
+            frames.append(g.out.numpy().copy())  # frame f-1 is complete once frame f was put
+    out = g.flush()
+    if rank == 0:
+        frames.append(out.numpy().copy())
+        q.put(np.stack(frames))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_pipelined_gather_three_frames():
+    from mirror_maze import Scene, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    world, H, W = 2, 9, 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, H, W, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    o = Oracle.from_scene(Scene.build(10, 0))
+    for f in range(3):
+        ref, _ = o.trace_tile(default_uniform(W, H, 0), make_ext(2, 3, 15, frame=f), 0, 0, W, H)
+        assert np.array_equal(frames[f].view(np.uint32), ref.view(np.uint32)), f
+
+
 @pytest.mark.parametrize("world,H", [(2, 12), (3, 10)])
 def test_gloo_row_sharded_frame_equals_single_rank(world, H):
     import sys
