@@ -520,7 +520,9 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         float rx = rand_pm1(p.seed), ry = rand_pm1(p.seed), rz = rand_pm1(p.seed);
         F3 rd = F3{rx, ry, rz};
         float len2 = dot3(rd, rd);
-        while (sqrtf(len2) > 1.0f) {                         // shaders.metal:316-318
+        // shaders.metal:316-318, length(r) > 1: RN(sqrt(x)) > 1 <=> x > 1 + 2^-23
+        // for every binary32 x (exhaustive check: scripts/verify_sqrt_gt1.c)
+        while (len2 > 0x1.000002p0f) {
             rx = rand_pm1(p.seed); ry = rand_pm1(p.seed); rz = rand_pm1(p.seed);
             rd = F3{rx, ry, rz};
             len2 = dot3(rd, rd);
