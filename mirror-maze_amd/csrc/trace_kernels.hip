@@ -286,19 +286,29 @@ template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, Scr
 // 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread),
 // 3 nodes + compact rect records in LDS, 4 top of the tree in LDS (the first
 // sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2,
-// 5 nodes in LDS + each path's T and L parked in LDS while it traverses.
+// 5 nodes in LDS + each path's T and L parked in LDS while it traverses,
+// 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same.
 template <bool kStats, int kLds, int kBlock, int kMinWaves, int kWW>
 __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
                                                                          float4* __restrict__ samples,
                                                                          unsigned long long* stats, uint32_t* err,
                                                                          uint32_t* work, uint32_t stack_slots) {
-    if constexpr (kLds == 4) {
+    if constexpr (kLds == 4 || kLds == 6) {
         extern __shared__ float4 lds_top[];
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds_top[i] = sc.nodes[i];
         __syncthreads();
         WpStack<kWW> st;
-        wp_dispatch<kStats, kWW>(sc, view(SplitNodes{lds_top, sc.nodes, sc.n_lds_f4}), st, job, samples, stats,
-                                      err, work);
+        const SplitNodes nodes{lds_top, sc.nodes, sc.n_lds_f4};
+        if constexpr (kLds == 6)
+            wp_dispatch<kStats, kWW>(sc, view(nodes, sc.recs), st, job, samples, stats, err, work);
+        else
+            wp_dispatch<kStats, kWW>(sc, view(nodes), st, job, samples, stats, err, work);
+    } else if constexpr (kLds == 7) {
+        extern __shared__ float4 lds_nodes7[];
+        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes7[i] = sc.nodes[i];
+        __syncthreads();
+        WpStack<kWW> st;
+        wp_dispatch<kStats, kWW>(sc, view(lds_nodes7, sc.recs), st, job, samples, stats, err, work);
     } else if constexpr (kLds > 0) {
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
@@ -334,7 +344,7 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        uint32_t stack_slots, hipStream_t s) {
     const uint32_t block = kBlock;
-    const size_t lds = kLds == 4 ? (size_t)sc.n_lds_f4 * sizeof(float4)
+    const size_t lds = (kLds == 4 || kLds == 6) ? (size_t)sc.n_lds_f4 * sizeof(float4)
                                  : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
                                        (kLds == 5 ? 6 * (size_t)block * sizeof(float) : 0) +
                                        (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
@@ -369,7 +379,7 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
         if (loop_form == 0) { MM_WP2(4, B, W, 0) }                                                    \
         if (loop_form == 2) { MM_WP2(4, B, W, 2) }                                                    \
         if (loop_form == 3) { MM_WP2(4, B, W, 3) }                                                    \
-        if (loop_form == 0) { MM_WP2(5, B, W, 0) }                                                    \
+        if (loop_form == 0) { MM_WP2(5, B, W, 0) MM_WP2(6, B, W, 0) MM_WP2(7, B, W, 0) }              \
         if (loop_form == 4) { MM_WP2(4, B, W, 4) MM_WP2(3, B, W, 4) MM_WP2(1, B, W, 4) MM_WP2(0, B, W, 4) }  \
         MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 2) MM_WP3(B, W, 3) MM_WP3(B, W, 8) MM_WP3(B, W, 16)  \
         MM_WP3(B, W, 32) }

@@ -54,6 +54,10 @@ for _b, _w in ((512, 6), (1024, 8), (1024, 1)):
     VARIANTS[f"br-ldsrec-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=1, ww=4)
     VARIANTS[f"br-lds-b{_b}-w{_w}"] = dict(pipe=1, persist=2, lds=1, block=_b, mw=_w, ls=0, lr=0, ww=4)
 VARIANTS["br-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=4)
+VARIANTS["split1-gr0"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, gr=0)
+VARIANTS["split1-gr1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, gr=1)
+VARIANTS["lds-gr1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, gr=1)
+VARIANTS["lds-gr0"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, gr=0)
 VARIANTS["rt-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=3)
 for _kb in (0, 1, 16, 32, 48, 64, 80):
     VARIANTS[f"wp-split{_kb}"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=_kb)
@@ -101,6 +105,8 @@ def main():
             r.set_option(6, v["ls"])
         if "mw" in v:
             r.set_option(MM_OPT_MIN_WAVES, v["mw"])
+        if "gr" in v:
+            r.set_option(11, v["gr"])
         if "cold" in v:
             r.set_option(10, v["cold"])
         if "split" in v:

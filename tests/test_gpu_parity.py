@@ -107,7 +107,7 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
     "persist-ldsrects-t63-b512-w6": (1, {1: 1, 3: 1, 4: 63, 2: 512, 5: 6}),
     "persist-lds-t16-b1024-w1": (1, {1: 1, 3: 1, 4: 16, 2: 1024, 5: 1, 8: 0}),
-    "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0, 8: 0}),
+    "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0, 8: 0, 11: 0}),
     "wavepersist-ldsrects": (1, {1: 1, 3: 2, 8: 1}),
     "wavepersist-ldsrects-b512-w6": (1, {1: 1, 3: 2, 8: 1, 2: 512, 5: 6}),
     "wavepersist-ldsstack": (1, {1: 1, 3: 2, 6: 1, 8: 0}),
@@ -124,6 +124,9 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "lean-split2kb": (1, {1: 1, 3: 2, 7: 2, 9: 2}),
     "regtop-ldsrects": (1, {1: 1, 3: 2, 7: 3, 8: 1}),
     "coldlds": (1, {1: 1, 3: 2, 10: 1}),
+    "lds-globalrects": (1, {1: 1, 3: 2, 8: 0, 11: 1}),
+    "split2kb-globalrects": (1, {1: 1, 3: 2, 9: 2, 11: 1}),
+    "split2kb-generalrects": (1, {1: 1, 3: 2, 9: 2, 11: 0}),
     "bouncerefill-ldsrects": (1, {1: 1, 3: 2, 7: 4, 8: 1}),
     "bouncerefill-global-b512-w6": (1, {1: 0, 3: 2, 7: 4, 2: 512, 5: 6}),
     "bouncerefill-split2kb": (1, {1: 1, 3: 2, 7: 4, 9: 2}),
@@ -281,8 +284,8 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}],
-                         ids=["auto-split", "split-off", "split-8kb", "global", "mega"])
+@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}],
+                         ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects"])
 def test_large_scene_top_of_tree_cache(gpu, opts):
     """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
     default kernel caches the top of the breadth-first node array in LDS and
