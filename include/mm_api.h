@@ -139,8 +139,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   0 off, 1 auto size (default), >1: always use a cache of this many KB */
 #define MM_OPT_COLD_LDS   10   /* wave-persistent kernel: 1 park each path's T and L in LDS while its ray
                                   traverses (frees registers; nodes in LDS, no rect records), 0 off (default) */
-#define MM_OPT_GLOBAL_RECTS 11 /* wave-persistent kernel: 1 leaf tests read the compact rect records through
-                                  L1/L2 when they are not staged in LDS (default), 0 the general test */
+#define MM_OPT_GLOBAL_RECTS 11 /* wave-persistent kernel, rect records not staged in LDS: leaf tests read the
+                                  compact records through L1/L2 -- 0 never (general test), 1 always,
+                                  2 with the split node cache only (default) */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Wait for all work queued by this context. */

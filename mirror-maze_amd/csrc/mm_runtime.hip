@@ -70,7 +70,8 @@ struct mm_ctx {
     bool opt_lds = true;
     uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto size, else KB
     bool opt_cold_lds = false;      // park T and L in LDS during traversal
-    bool opt_glob_rects = true;     // compact rect records via L1/L2 when they are not in LDS
+    int opt_glob_rects = 2;         // compact rect records via L1/L2: 0 never, 1 whenever not in LDS,
+                                    // 2 (auto) with the split node cache only (measured: C5 +3 %, C3 -2 %)
     uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
     // Megakernel form (measured on C3, profiles/r01_ab_*.txt): wave-persistent
     // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
@@ -315,7 +316,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
         case MM_OPT_COLD_LDS: c->opt_cold_lds = value != 0; return MM_OK;
-        case MM_OPT_GLOBAL_RECTS: c->opt_glob_rects = value != 0; return MM_OK;
+        case MM_OPT_GLOBAL_RECTS:
+            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "global rects must be 0, 1 or 2");
+            c->opt_glob_rects = value;
+            return MM_OK;
         case MM_OPT_LDS_SPLIT:
             if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
             c->opt_lds_split = (uint32_t)value;
@@ -589,7 +593,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
             if (lds_fits && c->opt_cold_lds && c->opt_ww == 0 && lds_cold <= (size_t)(160 * 1024) * block / 2048)
                 mode = 5;
-            if (mode == 1 && c->opt_ww == 0 && c->opt_glob_rects) mode = 7;
+            if (mode == 1 && c->opt_ww == 0 && c->opt_glob_rects == 1) mode = 7;
             DevScene sc = dev_scene(c);
             if (c->opt_lds && (c->opt_ww == 0 || c->opt_ww == 2 || c->opt_ww == 3 || c->opt_ww == 4) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
@@ -598,7 +602,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                 const size_t budget = c->opt_lds_split == 1 ? (size_t)(160 * 1024) * block / 2048
                                                             : (size_t)c->opt_lds_split * 1024;
                 sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
-                mode = (c->opt_ww == 0 && c->opt_glob_rects) ? 6 : 4;
+                mode = (c->opt_ww == 0 && c->opt_glob_rects != 0) ? 6 : 4;
             }
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
