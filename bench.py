@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--pipeline", default="auto", choices=["auto", "mega", "wave"])
+    p.add_argument("--contexts", type=int, default=0,
+                   help="renderer contexts (one stream each) that consecutive frames alternate over; "
+                        "0 = 1 on one GPU, 2 when the frame is split over ranks")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (approx)")
     return p.parse_args()
@@ -106,11 +109,14 @@ def main():
 
     from mirror_maze import MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, Renderer, Scene
     from mirror_maze import default_uniform, make_ext
+    from mirror_maze._lib import MM_OPT_TAIL_GATE
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torchrun (even with one rank) the frame goes through the RCCL gather path
+    distributed = "WORLD_SIZE" in os.environ and "MASTER_PORT" in os.environ
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -119,9 +125,20 @@ def main():
 
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[args.config]
     scene = Scene.build(maze_n, 0)
-    ren = Renderer(local)
-    ren.set_pipeline({"auto": MM_PIPE_AUTO, "mega": MM_PIPE_MEGAKERNEL, "wave": MM_PIPE_WAVEFRONT}[args.pipeline])
-    ren.upload_scene(scene)
+    # Frames alternate over `contexts` renderer contexts, each on its own
+    # library stream: frames are independent, so frame k+1's blocks fill the
+    # CUs that frame k's last waves leave idle (the per-frame tail that bounds
+    # strong scaling: profiles/r01_scaling_probe.txt).
+    n_ctx = args.contexts if args.contexts > 0 else (1 if world == 1 else 2)
+    rens = []
+    for _ in range(n_ctx):
+        r = Renderer(local)
+        r.set_pipeline({"auto": MM_PIPE_AUTO, "mega": MM_PIPE_MEGAKERNEL, "wave": MM_PIPE_WAVEFRONT}[args.pipeline])
+        r.upload_scene(scene)
+        if n_ctx > 1:
+            r.set_option(MM_OPT_TAIL_GATE, 1)
+        rens.append(r)
+    streams = [r.own_stream() for r in rens]
     u = default_uniform(W, H, 0)
 
     # rows r, r+world, ... (mirror_maze/dist.py); pad so every rank sends the same shape
@@ -129,53 +146,67 @@ def main():
 
     y0, y_stride, my_rows = row_shard(H, world, rank)
     frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
-    # one RCCL gather per frame, issued async and double-buffered so it overlaps
-    # the next frame's trace (mirror_maze/dist.py: FrameGatherer)
-    gatherer = FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf) if world > 1 else None
-    tile1 = torch.zeros((H, W, 4), dtype=torch.float32, device=dev) if world == 1 else None
+    # one RCCL gather per frame, issued async on the frame's stream into
+    # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
+    gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf, slots=max(2, len(rens)),
+                              assembly_stream=torch.cuda.Stream(dev))
+                if distributed else None)
+    tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in rens]
+    last = [0]
 
-    def step(frame, stats=False):
-        ext = make_ext(spp, bl, ml, frame=frame)
-        tile = gatherer.tile() if gatherer else tile1
-        _, st = ren.trace_tile(u, ext, 0, y0, W, my_rows, y_stride=y_stride, out=tile[:my_rows], stats=stats)
-        if gatherer:
-            gatherer.put()
-        else:
-            frame_buf.copy_(tile[:H])
+    def step(k, frame, stats=False):
+        slot = k % len(rens)
+        with torch.cuda.stream(streams[slot]):
+            tile = gatherer.tile() if gatherer else tiles1[slot]
+            _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
+                                          y_stride=y_stride, out=tile[:my_rows], stats=stats)
+            if gatherer:
+                gatherer.put()
+        last[0] = slot
         return st
 
     def drain():
         if gatherer:
             gatherer.flush()
+        torch.cuda.synchronize(dev)
+        if not gatherer:
+            frame_buf.copy_(tiles1[last[0]])
 
     for i in range(args.warmup):
-        step(10_000 + i)
+        step(i, 10_000 + i)
     drain()
-    ren.set_profiling(True)
-    ren.kernel_timing(reset=True)
-    if world > 1:
+    for r in rens:
+        r.set_profiling(True)
+        r.kernel_timing(reset=True)
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
-    drain()  # the last frame's gather + assembly is inside the timed region
+        step(i, i)
+    if gatherer:
+        gatherer.flush()  # the last frames' gathers + assembly are inside the timed region
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    k_ms, k_launches = ren.kernel_timing(reset=True)
-    ren.set_profiling(False)
+    drain()
+    k_ms = k_launches = 0
+    for r in rens:
+        ms, n = r.kernel_timing(reset=True)
+        r.set_profiling(False)
+        k_ms += ms
+        k_launches += n
 
     # count the rays of exactly the timed frames (deterministic re-run, untimed)
     rays = paths = visits = rtests = 0
     for i in range(args.steps):
-        st = step(i, stats=True)
+        st = step(i, i, stats=True)
         rays += st.rays; paths += st.paths; visits += st.node_visits; rtests += st.rect_tests
     drain()
     counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
     t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
     rays_all, paths_all, visits_all, rtests_all = (float(x) for x in counts.tolist())
@@ -211,13 +242,17 @@ def main():
             "data": "synthetic: Kruskal maze seed 0 (host C++ restatement), default camera, RNG keyed (pixel,sample,frame)",
             "config": {"workload": desc, "maze_n": maze_n, "width": W, "height": H, "spp": spp,
                        "bounce_limit": bl, "mirror_limit": ml, "pipeline": args.pipeline,
-                       "parallelism": f"rows interleaved x{world} + RCCL gather" if world > 1 else "1 GPU",
+                       "parallelism": f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU",
+                       "frame_contexts": len(rens),
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),
                        "node_visits_per_ray": round(visits_all / max(rays_all, 1), 2),
                        "rect_tests_per_ray": round(rtests_all / max(rays_all, 1), 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "trace", "kernel_avg_ms": round(k_avg_s * 1e3, 3), "launches": k_launches,
+                         "timing": ("HIP events around each launch on its stream" +
+                                    (f"; {len(rens)} contexts: consecutive launches overlap, so a launch's "
+                                     "span includes time shared with its neighbours" if len(rens) > 1 else "")),
                          "bytes_per_ray": BYTES_PER_RAY,
                          "valu": {"achieved_tops": round(valu_ops / k_avg_s / 1e12, 3), "peak_tops": VALU_PEAK_TOPS,
                                   "frac": round(valu_ops / k_avg_s / 1e12 / VALU_PEAK_TOPS, 4),
@@ -227,8 +262,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, u, make_ext(spp, bl, ml, frame=0), W, H, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    ren.close()
-    if world > 1:
+    for r in rens:
+        r.close()
+    if distributed:
         dist.destroy_process_group()
 
 

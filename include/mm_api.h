@@ -46,6 +46,9 @@ const char* mm_last_error(const mm_ctx* ctx);
  * MM_OWN_STREAM restores the context's own non-blocking stream. */
 #define MM_OWN_STREAM ((void*)(intptr_t)-1)
 int  mm_set_stream(mm_ctx* ctx, void* hip_stream);
+/* The stream work is enqueued on (after mm_set_stream; initially the
+ * context's own stream), e.g. to wrap it for torch.cuda.ExternalStream. */
+int  mm_get_stream(const mm_ctx* ctx, void** hip_stream);
 
 /* Replaces make_buf for buffers 1,2,3,5,6 (main.rs:725-730):
  *   rects      buffer 1  mirrors      n_rects x 48 B
@@ -127,10 +130,12 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   2: wave-persistent megakernel, 64-path chunks (default) */
 #define MM_OPT_THRESHOLD   4   /* persistent kernel: traverse while > N lanes traverse (0..63) */
 #define MM_OPT_MIN_WAVES   5   /* wave-persistent kernel register budget: 1, 6 or 8 (default) waves/SIMD */
-#define MM_OPT_TRAVERSAL   7   /* wave-persistent kernel loop form: 0 if-if (default), 1 while-while,
+#define MM_OPT_TRAVERSAL   7   /* wave-persistent kernel loop form: 0 if-if, 1 while-while,
                                   2 lean if-if (one pop site, no overflow test),
                                   3 if-if with the stack top in a register,
                                   4 if-if, lanes refilled with new paths at every bounce,
+                                  5 leaf tests and the next interior step in one iteration (1024/8 only),
+                                  -1 auto: 5 at 1024 threads / 8 waves, else 0 (default)
                                   8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
 #define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
 #define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 0 scratch (default) */
@@ -142,7 +147,22 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_GLOBAL_RECTS 11 /* wave-persistent kernel, rect records not staged in LDS: leaf tests read the
                                   compact records through L1/L2 -- 0 never (general test), 1 always,
                                   2 with the split node cache only (default) */
+#define MM_OPT_FUSE_RESOLVE 12 /* wave-persistent kernel: 1 reduce each pixel's samples inside the wave
+                                  that traced them when 64 % spp == 0 (default), 0 separate k_resolve */
+#define MM_OPT_TAIL_GATE  13  /* 1: queue a one-wave no-op ahead of every trace launch, so that when
+                                  several contexts' frames share the GPU a frame starts on the CUs the
+                                  previous frame's tail frees, not alongside it (0 default) */
+#define MM_OPT_FAIR       14  /* wave-persistent kernel: 1 raise the issue priority of waves behind the
+                                  mean chunk count (evens out per-wave progress), 0 default */
+#define MM_OPT_GRAB       15  /* wave-persistent kernel: 64-path chunks a wave claims per atomic on the
+                                  work counter, 1..16 (1 default) */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
+
+/* Diagnostics: record, for every wave of the wave-persistent kernel, four u64
+ * into the device buffer `dev_buf` (n_waves x 4): entry time, LDS staging
+ * done, exit time (wall_clock64 ticks, 100 MHz) and the number of 64-path
+ * chunks it traced.  NULL turns it off (default).  scripts/timeline_probe.py */
+int  mm_set_wave_timeline(mm_ctx* ctx, unsigned long long* dev_buf, uint32_t n_waves);
 
 /* Wait for all work queued by this context. */
 int  mm_sync(mm_ctx* ctx);

@@ -22,6 +22,18 @@ struct TileJob {
     mm_ext e;
     uint32_t x0, y0, w, h, y_stride;
     uint32_t view_w;     // (uint32_t)u.view_w — pixel index stride
+    // Fused resolve (wave-persistent kernel, 64 % spp == 0): each wave reduces
+    // its chunk's whole pixels in registers and writes out[pixel] itself, in
+    // k_resolve's order; no per-sample staging buffer, no resolve launch.
+    float4* out = nullptr;
+    uint32_t fuse = 0;
+    // Diagnostics (mm_set_wave_timeline): per wave of the wave-persistent
+    // kernel, 4 x u64 = (entry, LDS staged, exit, chunks) in wall_clock64()
+    // ticks (100 MHz).  Null = off.
+    unsigned long long* wave_ts = nullptr;
+    uint32_t wave_ts_cap = 0;
+    uint32_t fair = 0;   // MM_OPT_FAIR bits (wave-persistent kernel scheduling)
+    uint32_t grab = 1;   // 64-path chunks claimed per atomic (MM_OPT_GRAB)
 };
 
 struct MegaOpts {
@@ -37,7 +49,8 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
                              const MegaOpts& o, hipStream_t s);
 
 // Throughput mode, wave-persistent megakernel: resident blocks, waves pull
-// 64-path chunks from `work` (zeroed by the launcher).
+// 64-path chunks from work[0]; work[0..1] must be zero at launch and are left
+// zero by the kernel itself (the last wave re-zeroes them).
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
@@ -93,6 +106,9 @@ hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, ui
 hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,
                                 float4* out, hipStream_t s);
 hipError_t launch_quantize(const float4* in, uint32_t* out, size_t n, hipStream_t s);
+
+// One-wave no-op ahead of a trace launch (MM_OPT_TAIL_GATE, trace_kernels.hip).
+hipError_t launch_tail_gate(hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);

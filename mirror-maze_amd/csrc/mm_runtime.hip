@@ -77,10 +77,17 @@ struct mm_ctx {
     // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
     int opt_persist = 2;         // 0 one thread per path, 1 lane refill, 2 wave-persistent
     uint32_t opt_min_waves = 8;  // wave-persistent launch bound (waves per SIMD)
-    int opt_ww = 0;              // traversal loop: 0 if-if, 1 while-while, 8/16/32 leaf batch
+    int opt_ww = -1;             // traversal loop: -1 auto (5 at 1024/8, else 0), 0 if-if, 1 while-while,
+                                 // 5 leaf+interior per iteration, 8/16/32 leaf batch
     int opt_lds_rects = 1;       // compact rect records in LDS next to the BVH when they fit
     int opt_lds_stack = 0;       // u16 LDS stack: measured equal to scratch (profiles/r01_ab_ldsstack.txt)
     uint32_t opt_threshold = 32;
+    bool opt_fuse = true;
+    bool opt_tail_gate = false;
+    uint32_t opt_fair = 0;       // MM_OPT_FAIR bits
+    uint32_t opt_grab = 1;       // chunks per work-counter atomic
+    unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
+    uint32_t wave_ts_cap = 0;  // one-wave no-op ahead of each trace launch (contexts sharing the GPU)        // resolve fused into the wave-persistent kernel when 64 % spp == 0
     // per-kernel profiling of the trace kernel (mm_set_profiling)
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
@@ -226,7 +233,10 @@ int read_aux(mm_ctx* c, mm_stats* st) {
     HIPC(c, hipMemcpyAsync(h, c->d_aux, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     if (st) { st->rays = h[0]; st->node_visits = h[1]; st->rect_tests = h[2]; st->paths = h[3]; }
-    if ((uint32_t)h[4] != 0) return fail(c, MM_ERR_STACK, "traversal stack overflow (depth > 50)");
+    if ((uint32_t)h[4] != 0) {
+        HIPC(c, hipMemsetAsync(c->d_aux + 4, 0, sizeof(unsigned long long), c->stream));
+        return fail(c, MM_ERR_STACK, "traversal stack overflow (depth > 50)");
+    }
     return MM_OK;
 }
 
@@ -288,6 +298,19 @@ int mm_set_stream(mm_ctx* c, void* s) {
     return MM_OK;
 }
 
+int mm_set_wave_timeline(mm_ctx* c, unsigned long long* buf, uint32_t n_waves) {
+    if (!c) return MM_ERR_INVALID;
+    c->d_wave_ts = n_waves ? buf : nullptr;
+    c->wave_ts_cap = buf ? n_waves : 0;
+    return MM_OK;
+}
+
+int mm_get_stream(const mm_ctx* c, void** s) {
+    if (!c || !s) return MM_ERR_INVALID;
+    *s = (void*)c->stream;
+    return MM_OK;
+}
+
 int mm_set_pipeline(mm_ctx* c, int pipe) {
     if (!c) return MM_ERR_INVALID;
     if (pipe < MM_PIPE_AUTO || pipe > MM_PIPE_REFERENCE) return fail(c, MM_ERR_INVALID, "unknown pipeline");
@@ -309,12 +332,22 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_LDS_STACK: c->opt_lds_stack = value != 0; return MM_OK;
         case MM_OPT_TRAVERSAL:
-            if (value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 8 && value != 16 &&
-                value != 32)
-                return fail(c, MM_ERR_INVALID, "traversal loop form must be 0, 1, 2, 3, 4, 8, 16 or 32");
+            if (value != -1 && value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 5 &&
+                value != 8 && value != 16 && value != 32)
+                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0, 1, 2, 3, 4, 5, 8, 16 or 32");
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
+        case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
+        case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
+        case MM_OPT_GRAB:
+            if (value < 1 || value > 16) return fail(c, MM_ERR_INVALID, "grab must be 1..16");
+            c->opt_grab = (uint32_t)value;
+            return MM_OK;
+        case MM_OPT_FAIR:
+            if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "fair must be 0 or 1");
+            c->opt_fair = (uint32_t)value;
+            return MM_OK;
         case MM_OPT_COLD_LDS: c->opt_cold_lds = value != 0; return MM_OK;
         case MM_OPT_GLOBAL_RECTS:
             if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "global rects must be 0, 1 or 2");
@@ -462,7 +495,7 @@ int mm_trace_chunks(mm_ctx* c, const mm_uniform* u, const uint32_t* chunks, uint
     if (rc) return rc;
     HIPC(c, hipMemcpyAsync(c->d_chunks, chunks, 2 * (size_t)n_chunks * sizeof(uint32_t), hipMemcpyHostToDevice,
                            c->stream));
-    HIPC(c, hipMemsetAsync(c->d_aux, 0, 8 * sizeof(unsigned long long), c->stream));
+    HIPC(c, hipMemsetAsync(c->d_aux, 0, 5 * sizeof(unsigned long long), c->stream));  // stats, error flag
     if ((rc = begin_timing(c))) return rc;
     HIPC(c, launch_trace_chunks(dev_scene(c), *u, c->d_chunks, gw, gh, c->d_fb, c->d_fb8, c->d_aux,
                                 reinterpret_cast<uint32_t*>(c->d_aux + 4), false, c->stream));
@@ -540,9 +573,16 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
     const uint64_t batch_paths = wave ? (32ull << 20) : (64ull << 20);
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
-    int rc = ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
+    // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
+    const bool fuse = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_ww != 4 &&
+                      c->opt_fuse && 64 % e->spp == 0;
+    int rc = fuse ? MM_OK : ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
     if (rc) return rc;
-    HIPC(c, hipMemsetAsync(c->d_aux, 0, 8 * sizeof(unsigned long long), c->stream));
+    // aux: [0..3] stats (zeroed only when counted), [4] sticky error flag
+    // (cleared by read_aux), [5] lane-refill counter (zeroed by its launcher),
+    // [6] wave-persistent counter pair (self-cleaning).  No fill kernel on the
+    // default path: see k_trace_wavepersist.
+    if (want_stats) HIPC(c, hipMemsetAsync(c->d_aux, 0, 4 * sizeof(unsigned long long), c->stream));
     if ((rc = begin_timing(c))) return rc;
     uint32_t launches = 0;
     for (uint32_t j0 = 0; j0 < h; j0 += rows_per_batch) {
@@ -555,6 +595,13 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         job.h = std::min(rows_per_batch, h - j0);
         job.y_stride = y_stride;
         job.view_w = W;
+        job.fuse = fuse ? 1u : 0u;
+        job.wave_ts = c->d_wave_ts;
+        job.fair = c->opt_fair;
+        job.grab = c->opt_grab;
+        job.wave_ts_cap = c->wave_ts_cap;
+        job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
+        if (c->opt_tail_gate) HIPC(c, launch_tail_gate(c->stream));
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
         if (wave) {
@@ -583,31 +630,35 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             if (!inst)
                 return fail(c, MM_ERR_UNSUPPORTED, "wave-persistent kernel: block/min-waves pair not instantiated "
                                                    "(256/8, 512/6, 512/8, 1024/1, 1024/8)");
+            // loop form: auto = leaf+interior per iteration (measured 10.35 vs 11.06 ms on C3,
+            // profiles/r01_ab_leafinterior.txt) where it is instantiated, else if-if
+            const int ww = c->opt_ww >= 0 ? c->opt_ww
+                                          : ((block == 1024 && c->opt_min_waves == 8 && !c->opt_cold_lds) ? 5 : 0);
             const uint32_t slots = std::max(1u, c->depth);
             // keep 2 blocks of 1024 (or their equivalent) resident: <= 80 KB of LDS per block
             const size_t lds_total = 2 * (size_t)c->n_nodes * sizeof(float4) + (size_t)slots * block * 2;
             const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= (size_t)(160 * 1024) * block / 2048;
             const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
             const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * block / 2048;
-            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && c->opt_ww != 4 ? 2 : 1)) : 0;
+            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && ww != 4 ? 2 : 1)) : 0;
             const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
-            if (lds_fits && c->opt_cold_lds && c->opt_ww == 0 && lds_cold <= (size_t)(160 * 1024) * block / 2048)
+            if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= (size_t)(160 * 1024) * block / 2048)
                 mode = 5;
-            if (mode == 1 && c->opt_ww == 0 && c->opt_glob_rects == 1) mode = 7;
+            if (mode == 1 && (ww == 0 || ww == 5) && c->opt_glob_rects == 1) mode = 7;
             DevScene sc = dev_scene(c);
-            if (c->opt_lds && (c->opt_ww == 0 || c->opt_ww == 2 || c->opt_ww == 3 || c->opt_ww == 4) &&
+            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
                 // nodes exceed the LDS budget (or an explicit cache size is set):
                 // cache the top of the breadth-first array
                 const size_t budget = c->opt_lds_split == 1 ? (size_t)(160 * 1024) * block / 2048
                                                             : (size_t)c->opt_lds_split * 1024;
                 sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
-                mode = (c->opt_ww == 0 && c->opt_glob_rects != 0) ? 6 : 4;
+                mode = ((ww == 0 || ww == 5) && c->opt_glob_rects != 0) ? 6 : 4;
             }
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
-                                             reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, mode, slots,
-                                             block, c->opt_min_waves, c->opt_ww, c->stream));
+                                             reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, slots,
+                                             block, c->opt_min_waves, ww, c->stream));
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
             PersistOpts po;
             po.block = c->opt_block ? c->opt_block : 1024u;
@@ -631,6 +682,10 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                                       reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
         }
         if ((rc = prof_mark(c))) return rc;
+        if (fuse) {
+            launches += 1;
+            continue;
+        }
         HIPC(c, launch_resolve(job, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
         launches += 2;
     }

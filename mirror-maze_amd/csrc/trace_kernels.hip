@@ -148,12 +148,47 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
 }
 
+// The per-pixel reduction of k_resolve done inside a wave: with 64 % spp == 0
+// and chunks starting at multiples of 64, a wave's 64 paths are 64/spp whole
+// pixels (lanes [p*spp, (p+1)*spp)).  spp % 8 == 0: pairwise tree in blocks of
+// 8 by xor-shuffles (a+b == b+a exactly), blocks added left to right by the
+// pixel's first lane; otherwise a left-to-right sum.  Then / spp -- the same
+// operations in the same order as k_resolve, so the pixel is bit-identical.
+// Called by all 64 lanes (uniform control flow); `valid` lanes' pixels written.
+__device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32_t path, bool valid) {
+    const uint32_t spp = job.e.spp, lane = threadIdx.x & 63u;
+    F3 acc;
+    if (spp % 8 == 0) {
+        s = s + F3{__shfl_xor(s.x, 1), __shfl_xor(s.y, 1), __shfl_xor(s.z, 1)};
+        s = s + F3{__shfl_xor(s.x, 2), __shfl_xor(s.y, 2), __shfl_xor(s.z, 2)};
+        s = s + F3{__shfl_xor(s.x, 4), __shfl_xor(s.y, 4), __shfl_xor(s.z, 4)};
+        acc = s;
+        for (uint32_t b = 8; b < spp; b += 8)
+            acc = acc + F3{__shfl(s.x, (int)(lane + b)), __shfl(s.y, (int)(lane + b)), __shfl(s.z, (int)(lane + b))};
+    } else {
+        acc = s;
+        for (uint32_t k = 1; k < spp; ++k)
+            acc = acc + F3{__shfl(s.x, (int)(lane + k)), __shfl(s.y, (int)(lane + k)), __shfl(s.z, (int)(lane + k))};
+    }
+    if (valid && (lane & (spp - 1)) == 0) {
+        const uint32_t pix = path / spp;
+        const float m = (float)spp;
+        const F3 v = F3{acc.x / m, acc.y / m, acc.z / m};
+        if (job.e.flags & MM_EXT_ACCUMULATE) {
+            const float4 o = job.out[pix];
+            job.out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
+        } else {
+            job.out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
+        }
+    }
+}
+
 // Wave-persistent megakernel: resident blocks (LDS filled once per block);
 // each wave takes 64 consecutive paths at a time from a global counter and
 // traces them exactly like k_trace_mega, so no block waits for its slowest
 // wave before the CU can take more work.
 template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
-__device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v, Stack& stack,
+__device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V& v, Stack& stack,
                                                  const TileJob& job, float4* __restrict__ samples,
                                                  unsigned long long* stats, uint32_t* err, uint32_t* work,
                                                  const Cold& cold = Cold{}) {
@@ -162,28 +197,51 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v,
     const uint32_t lane = threadIdx.x & 63u;
     const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
     Counters c;
-    uint32_t paths = 0;
+    uint32_t paths = 0, chunks = 0;
+    const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t grab = 64u * job.grab;   // paths claimed per atomic (MM_OPT_GRAB chunks)
+    uint32_t next = 0, end = 0;             // wave-uniform claimed range
     for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(work, 64u);
-        base = __shfl(base, 0);
+        if (next >= end) {
+            uint32_t b = 0;
+            if (lane == 0) b = atomicAdd(work, grab);
+            next = __builtin_amdgcn_readfirstlane(b);
+            end = min(next + grab, n_paths);
+        }
+        const uint32_t base = next;
+        next += 64u;
         if (base >= n_paths) break;
+        // MM_OPT_FAIR: a wave behind the mean chunk count runs at raised issue
+        // priority (the SIMD arbiter otherwise favours the oldest waves: chunk
+        // counts per wave spread 9-59 on C3, 28-37 with this on; the frame time
+        // does not change -- profiles/r01_timeline_probe.txt).
+        if (job.fair) {
+            if (__builtin_amdgcn_readfirstlane((uint64_t)chunks * n_waves < base / 64u ? 1u : 0u))
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+        ++chunks;
         const uint32_t path = base + lane;
-        if (path < n_paths) {
+        const bool valid = path < n_paths;
+        F3 s = F3{0.0f, 0.0f, 0.0f};
+        if (valid) {
             const uint32_t pix = path / spp, smp = path - pix * spp;
             const uint32_t j = pix / job.w, i = pix - j * job.w;
             const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
             uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
             const F3 d = jitter(primary_dir(job.u, px, py), seed);
             bool overflow = false;
-            const F3 s = trace_path<kStats, false, V, Stack, kWW>(sc, v, ori, d, seed, (int)job.e.bounce_limit,
-                                                                  (int)job.e.mirror_limit, stack, c, overflow, cold);
+            s = trace_path<kStats, false, V, Stack, kWW>(sc, v, ori, d, seed, (int)job.e.bounce_limit,
+                                                         (int)job.e.mirror_limit, stack, c, overflow, cold);
             if (overflow) atomicOr(err, 1u);
-            samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
+            if (!job.fuse) samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
         }
+        if (job.fuse) resolve_in_wave(job, s, path, valid);
     }
     if (kStats) flush_stats(stats, c, paths);
+    return chunks;
 }
 
 // Bounce-refill form of the wave-persistent body (loop form 4): a lane whose
@@ -192,7 +250,7 @@ __device__ __forceinline__ void wavepersist_body(const DevScene& sc, const V& v,
 // runs one bounce (closest hit + shade) per iteration for all lanes; every
 // path's operation sequence is trace_path's, so samples are bit-identical.
 template <bool kStats, typename V, typename Stack, typename Cold = NoCold>
-__device__ __forceinline__ void bouncerefill_body(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
+__device__ __forceinline__ uint32_t bouncerefill_body(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
                                                   float4* __restrict__ samples, unsigned long long* stats,
                                                   uint32_t* err, uint32_t* work) {
     const uint32_t spp = job.e.spp;
@@ -268,14 +326,15 @@ __device__ __forceinline__ void bouncerefill_body(const DevScene& sc, const V& v
         }
     }
     if (kStats) flush_stats(stats, c, paths);
+    return 0;
 }
 
 template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
-__device__ __forceinline__ void wp_dispatch(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
-                                            float4* __restrict__ samples, unsigned long long* stats, uint32_t* err,
-                                            uint32_t* work, const Cold& cold = Cold{}) {
-    if constexpr (kWW == 4) bouncerefill_body<kStats>(sc, v, stack, job, samples, stats, err, work);
-    else wavepersist_body<kStats, kWW>(sc, v, stack, job, samples, stats, err, work, cold);
+__device__ __forceinline__ uint32_t wp_dispatch(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
+                                                float4* __restrict__ samples, unsigned long long* stats,
+                                                uint32_t* err, uint32_t* work, const Cold& cold = Cold{}) {
+    if constexpr (kWW == 4) return bouncerefill_body<kStats>(sc, v, stack, job, samples, stats, err, work);
+    else return wavepersist_body<kStats, kWW>(sc, v, stack, job, samples, stats, err, work, cold);
 }
 
 // Traversal stack of the wave-persistent kernel: loop form 3 is the if-if loop
@@ -288,27 +347,40 @@ template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, Scr
 // sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2,
 // 5 nodes in LDS + each path's T and L parked in LDS while it traverses,
 // 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same.
+// Diagnostics: time at which the block's LDS staging completed (wave timeline).
+#define MM_TS_STAGED()                                                                                      \
+    do {                                                                                                     \
+        if (job.wave_ts && (threadIdx.x & 63u) == 0) {                                                       \
+            const uint32_t wid_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                      \
+            if (wid_ < job.wave_ts_cap) job.wave_ts[4 * wid_ + 1] = (unsigned long long)wall_clock64();     \
+        }                                                                                                    \
+    } while (0)
+
 template <bool kStats, int kLds, int kBlock, int kMinWaves, int kWW>
 __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
                                                                          float4* __restrict__ samples,
                                                                          unsigned long long* stats, uint32_t* err,
                                                                          uint32_t* work, uint32_t stack_slots) {
+    const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
+    uint32_t chunks = 0;
     if constexpr (kLds == 4 || kLds == 6) {
         extern __shared__ float4 lds_top[];
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds_top[i] = sc.nodes[i];
         __syncthreads();
+        MM_TS_STAGED();
         WpStack<kWW> st;
         const SplitNodes nodes{lds_top, sc.nodes, sc.n_lds_f4};
         if constexpr (kLds == 6)
-            wp_dispatch<kStats, kWW>(sc, view(nodes, sc.recs), st, job, samples, stats, err, work);
+            chunks = wp_dispatch<kStats, kWW>(sc, view(nodes, sc.recs), st, job, samples, stats, err, work);
         else
-            wp_dispatch<kStats, kWW>(sc, view(nodes), st, job, samples, stats, err, work);
+            chunks = wp_dispatch<kStats, kWW>(sc, view(nodes), st, job, samples, stats, err, work);
     } else if constexpr (kLds == 7) {
         extern __shared__ float4 lds_nodes7[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes7[i] = sc.nodes[i];
         __syncthreads();
+        MM_TS_STAGED();
         WpStack<kWW> st;
-        wp_dispatch<kStats, kWW>(sc, view(lds_nodes7, sc.recs), st, job, samples, stats, err, work);
+        chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes7, sc.recs), st, job, samples, stats, err, work);
     } else if constexpr (kLds > 0) {
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
@@ -316,26 +388,47 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
         if constexpr (kLds == 3)
             for (uint32_t i = threadIdx.x; i < 5 * sc.n_rects; i += blockDim.x) lds_recs[i] = sc.recs[i];
         __syncthreads();
+        MM_TS_STAGED();
         if constexpr (kLds == 3) {
             WpStack<kWW> st;
-            wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
+            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
         } else if constexpr (kLds == 5) {
             WpStack<kWW> st;
             const LdsCold cold{reinterpret_cast<float*>(lds_recs) + threadIdx.x, blockDim.x};
-            wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work, cold);
+            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work, cold);
         } else if constexpr (kLds == 2) {
             LdsStack16 st;
             st.base = reinterpret_cast<uint16_t*>(lds_recs) + threadIdx.x;
             st.stride = blockDim.x;
             st.cap = stack_slots;
-            wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         } else {
             WpStack<kWW> st;
-            wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         }
     } else {
         WpStack<kWW> st;
-        wp_dispatch<kStats, kWW>(sc, view(sc.nodes), st, job, samples, stats, err, work);
+        chunks = wp_dispatch<kStats, kWW>(sc, view(sc.nodes), st, job, samples, stats, err, work);
+    }
+    if (job.wave_ts && (threadIdx.x & 63u) == 0) {
+        const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (wid < job.wave_ts_cap) {
+            job.wave_ts[4 * wid + 0] = t_entry;
+            job.wave_ts[4 * wid + 2] = (unsigned long long)wall_clock64();
+            job.wave_ts[4 * wid + 3] = chunks;
+        }
+    }
+    // Self-cleaning work counter (work[0] = next path, work[1] = waves done):
+    // the last wave to finish re-zeroes both, so the next launch needs no
+    // memset -- a fill kernel queued between two frames on another stream
+    // would wait for free CUs and serialise overlapping frames.
+    if ((threadIdx.x & 63u) == 0) {
+        __threadfence();
+        const uint32_t total = gridDim.x * (blockDim.x >> 6);
+        if (atomicAdd(work + 1, 1u) == total - 1) {
+            atomicExch(work, 0u);
+            atomicExch(work + 1, 0u);
+        }
     }
 }
 
@@ -359,8 +452,6 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     const uint32_t n_paths = job.w * job.h * job.e.spp;
     uint32_t grid = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus);
     grid = std::max(1u, std::min(grid, (n_paths + block - 1) / block));
-    e = hipMemsetAsync(work, 0, sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, s, sc, job, samples, stats, err, work, stack_slots);
     return hipGetLastError();
 }
@@ -384,6 +475,9 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
         MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 2) MM_WP3(B, W, 3) MM_WP3(B, W, 8) MM_WP3(B, W, 16)  \
         MM_WP3(B, W, 32) }
     MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
+    if (block == 1024 && min_waves == 8 && loop_form == 5) {
+        MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP3(1024, 8, 5)
+    }
 #undef MM_WP
 #undef MM_WP3
 #undef MM_WP2
@@ -410,6 +504,20 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
         launch_mega_t<false, true>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
     else
         launch_mega_t<false, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Tail gate: a one-wave no-op queued ahead of a frame's trace kernel when
+// frames from several contexts share the GPU.  It can only be dispatched once
+// a wave slot frees up, i.e. once the frame already running starts to drain,
+// so the next frame's resident blocks fill exactly the CUs the previous
+// frame's tail leaves idle instead of splitting the GPU with it from the start
+// (measured: profiles/r01_overlap_probe.txt).
+__global__ void k_tail_gate() {}
+
+hipError_t launch_tail_gate(hipStream_t s) {
+    hipLaunchKernelGGL(k_tail_gate, dim3(1), dim3(64), 0, s);
     return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE = 0x1, 0x2
 MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2, 3
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_THRESHOLD, MM_OPT_MIN_WAVES, MM_OPT_LDS_STACK = 1, 2, 3, 4, 5, 6
 MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS, MM_OPT_LDS_SPLIT, MM_OPT_COLD_LDS, MM_OPT_GLOBAL_RECTS = 7, 8, 9, 10, 11
+MM_OPT_FUSE_RESOLVE, MM_OPT_TAIL_GATE, MM_OPT_FAIR = 12, 13, 14
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
 
@@ -88,6 +89,7 @@ EXPORTS = {
     "mm_destroy": (None, [P]),
     "mm_last_error": (C.c_char_p, [P]),
     "mm_set_stream": (C.c_int, [P, P]),
+    "mm_get_stream": (C.c_int, [P, C.POINTER(P)]),
     "mm_upload_scene": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32, P, P, P]),
     "mm_trace_chunks": (C.c_int, [P, C.POINTER(mm_uniform), P, C.c_uint32]),
     "mm_read_framebuffer": (C.c_int, [P, P, P]),
@@ -98,6 +100,7 @@ EXPORTS = {
                                 C.c_uint32, C.c_uint32, C.c_uint32, P, C.POINTER(mm_stats)]),
     "mm_set_pipeline": (C.c_int, [P, C.c_int]),
     "mm_set_option": (C.c_int, [P, C.c_int, C.c_int]),
+    "mm_set_wave_timeline": (C.c_int, [P, P, C.c_uint32]),
     "mm_sync": (C.c_int, [P]),
     "mm_last_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
     "mm_set_profiling": (C.c_int, [P, C.c_int]),

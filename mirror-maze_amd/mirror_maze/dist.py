@@ -56,55 +56,93 @@ def gather_frame(tile, height: int, dst: int = 0, group=None, out=None):
 class FrameGatherer:
     """Pipelined frame-end gather for a sequence of frames.
 
-    Two tile buffers alternate: frame k is traced into ``tile(k)`` and its
-    gather is issued asynchronously, so it runs on the collective's stream
-    while frame k+1 is traced; the assembly of frame k on rank ``dst`` is
-    queued after frame k+1's trace (``put`` of frame k+1 waits for gather k
-    before assembling it).  ``flush`` completes the last frame.  Stream order
-    makes the reuse safe: gather k is awaited (on the current stream) before
-    frame k+2 is traced into the same tile, and every gather is launched after
-    the current stream's earlier work (the assembly reading its buffers)."""
+    ``slots`` tile buffers rotate: frame k is traced into ``tile()`` (slot
+    k % slots) and ``put()`` issues its gather asynchronously on the current
+    stream, so the collective runs while later frames are traced.  The gather
+    of frame k is completed -- awaited on the current stream, then assembled
+    on rank ``dst`` -- when its slot is handed out again (``tile()`` of frame
+    k + slots) or by ``flush()``.  A caller that traces frame k on stream
+    s[k % slots] (bench.py: one renderer context per stream, so consecutive
+    frames overlap on the GPU) calls ``tile()`` and ``put()`` inside that
+    stream; then each stream waits only for the gather that last read its own
+    tile before overwriting it, and never for the other stream's trace.
+    Completed frames are copied into ``out`` and passed to ``on_frame(k,
+    frame)`` (rank ``dst`` only), in frame order.  With ``assembly_stream``
+    (CUDA only) the de-interleave runs there instead of on the trace streams:
+    a small copy kernel queued ahead of a trace kernel would wait for the CUs
+    the other stream's trace holds and delay that trace."""
 
-    def __init__(self, shape, height: int, device, dst: int = 0, group=None, out=None):
+    def __init__(self, shape, height: int, device, dst: int = 0, group=None, out=None, slots: int = 2,
+                 on_frame=None, assembly_stream=None):
         import torch
         import torch.distributed as dist
 
         self.height, self.dst, self.group, self.out = height, dst, group, out
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.tiles = [torch.zeros(shape, dtype=torch.float32, device=device) for _ in range(2)]
+        self.slots = slots
+        self.on_frame = on_frame
+        self.tiles = [torch.zeros(shape, dtype=torch.float32, device=device) for _ in range(slots)]
         self.bufs = ([[torch.empty(shape, dtype=torch.float32, device=device) for _ in range(self.world)]
-                      for _ in range(2)] if self.rank == dst else [None, None])
+                      for _ in range(slots)] if self.rank == dst else [None] * slots)
         self.k = 0
-        self.pending = None
+        self.pending = [None] * slots   # (frame index, Work) per slot
+        self.asm = assembly_stream
+        self.asm_done = [None] * slots  # event: assembly of the slot's last frame done
 
     def tile(self):
-        """The buffer the next frame must be traced into."""
-        return self.tiles[self.k % 2]
+        """The buffer the next frame must be traced into (completes the gather
+        that last used it)."""
+        slot = self.k % self.slots
+        self._finish(slot)
+        return self.tiles[slot]
 
     def put(self):
         """Issue the gather of the frame just traced into ``tile()``."""
         import torch.distributed as dist
 
-        slot = self.k % 2
+        slot = self.k % self.slots
+        if self.asm_done[slot] is not None:  # bufs[slot] is free once its last assembly ran
+            import torch
+
+            torch.cuda.current_stream().wait_event(self.asm_done[slot])
+            self.asm_done[slot] = None
         work = dist.gather(self.tiles[slot], self.bufs[slot], dst=self.dst, group=self.group, async_op=True)
-        prev, self.pending = self.pending, (work, slot)
+        self.pending[slot] = (self.k, work)
         self.k += 1
-        if prev is not None:
-            self._finish(prev)
 
     def flush(self):
-        if self.pending is not None:
-            prev, self.pending = self.pending, None
-            self._finish(prev)
+        """Complete every outstanding gather (oldest first); returns ``out``."""
+        for i in range(self.slots):
+            self._finish((self.k + i) % self.slots)
         return self.out
 
-    def _finish(self, p):
-        work, slot = p
-        work.wait()
-        if self.rank == self.dst:
-            frame = assemble(self.bufs[slot], self.height)
-            if self.out is None:
-                self.out = frame.clone()
-            else:
-                self.out.copy_(frame)
+    def _finish(self, slot):
+        p = self.pending[slot]
+        if p is None:
+            return
+        self.pending[slot] = None
+        k, work = p
+        work.wait()  # the current stream may now overwrite tiles[slot]
+        if self.rank != self.dst:
+            return
+        if self.asm is None:
+            self._assemble(k, slot)
+            return
+        import torch
+
+        with torch.cuda.stream(self.asm):
+            work.wait()
+            self._assemble(k, slot)
+            ev = torch.cuda.Event()
+            ev.record(self.asm)
+            self.asm_done[slot] = ev
+
+    def _assemble(self, k, slot):
+        frame = assemble(self.bufs[slot], self.height)
+        if self.out is None:
+            self.out = frame.clone()
+        else:
+            self.out.copy_(frame)
+        if self.on_frame is not None:
+            self.on_frame(k, self.out)

@@ -58,6 +58,28 @@ class Renderer:
         handle = _lib.MM_OWN_STREAM if stream is None else int(getattr(stream, "cuda_stream", stream))
         self._check(lib().mm_set_stream(self._ctx, handle))
 
+    def own_stream(self):
+        """Pin the context's own (library-created, non-blocking) stream and
+        return it as a torch.cuda.ExternalStream, so torch ops can be ordered
+        with this context's work.  Two contexts on their own streams run
+        independent frames concurrently (the next frame's blocks fill the
+        CUs the previous frame's tail leaves idle)."""
+        import torch
+
+        self.set_stream(_lib.MM_OWN_STREAM)
+        h = C.c_void_p()
+        self._check(lib().mm_get_stream(self._ctx, C.byref(h)))
+        return torch.cuda.ExternalStream(h.value, device=torch.device(f"cuda:{self.device}"))
+
+    def set_wave_timeline(self, buf=None) -> None:
+        """Diagnostics: per-wave (entry, staged, exit, chunks) u64 records of
+        the wave-persistent kernel into an int64 CUDA tensor of shape
+        (n_waves, 4); None turns recording off."""
+        if buf is None:
+            self._check(lib().mm_set_wave_timeline(self._ctx, None, 0))
+        else:
+            self._check(lib().mm_set_wave_timeline(self._ctx, buf.data_ptr(), buf.shape[0]))
+
     def set_pipeline(self, pipe: int) -> None:
         self._check(lib().mm_set_pipeline(self._ctx, pipe))
 

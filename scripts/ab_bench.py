@@ -59,6 +59,15 @@ VARIANTS["split1-gr1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=
 VARIANTS["lds-gr1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, gr=1)
 VARIANTS["lds-gr0"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, gr=0)
 VARIANTS["rt-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=3)
+VARIANTS["default"] = dict(pipe=1)  # library defaults (auto loop form, fused resolve)
+VARIANTS["nofuse"] = dict(pipe=1, fuse=0)
+for _f in (1,):
+    VARIANTS[f"fair{_f}"] = dict(pipe=1, fair=_f)
+for _g in (2, 4, 8):
+    VARIANTS[f"grab{_g}"] = dict(pipe=1, grab=_g)
+VARIANTS["li-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=5)
+VARIANTS["li-lds"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, ww=5)
+VARIANTS["li-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=5)
 for _kb in (0, 1, 16, 32, 48, 64, 80):
     VARIANTS[f"wp-split{_kb}"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=_kb)
     VARIANTS[f"wp-split{_kb}-b512-w6"] = dict(pipe=1, persist=2, lds=1, block=512, mw=6, split=_kb)
@@ -101,6 +110,14 @@ def main():
             r.set_option(8, v["lr"])
         if "ww" in v:
             r.set_option(7, v["ww"])
+        elif v.get("persist") == 2:
+            r.set_option(7, 0)  # historical wp-* variants: the if-if loop
+        if "grab" in v:
+            r.set_option(15, v["grab"])
+        if "fair" in v:
+            r.set_option(14, v["fair"])
+        if "fuse" in v:
+            r.set_option(12, v["fuse"])
         if "ls" in v:
             r.set_option(6, v["ls"])
         if "mw" in v:

@@ -1,0 +1,68 @@
+#!/usr/bin/env python
+"""Per-wave timeline of the wave-persistent kernel (diagnostics): for rank 0's
+row set at N = 1, 2, 4, 8 (rows 0, N, 2N, ...) record every wave's entry,
+LDS-staged and exit times and its chunk count (mm_set_wave_timeline), and
+report where a launch's time goes: dispatch ramp, staging, steady state, and
+the tail between the first and the last wave to run out of work.
+
+    python scripts/timeline_probe.py [--config c3] [--ranks 1,2,4,8]
+"""
+import argparse
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "mirror-maze_amd"))
+
+
+def main():
+    import numpy as np
+    import torch
+
+    from bench import CONFIGS
+    from mirror_maze import Renderer, Scene, default_uniform, make_ext
+    from mirror_maze.dist import row_shard
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--fair", default="0", help="comma list of MM_OPT_FAIR values to compare")
+    ap.add_argument("--grab", type=int, default=1)
+    a = ap.parse_args()
+    maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
+    r = Renderer(0)
+    r.upload_scene(Scene.build(maze_n, 0))
+    u = default_uniform(W, H, 0)
+    ts = torch.zeros((65536, 4), dtype=torch.int64, device="cuda")
+    print(f"# {desc}; times in us (wall_clock64, 100 MHz)")
+    for fair, n in [(int(f), int(x)) for f in a.fair.split(",") for x in a.ranks.split(",")]:
+        r.set_option(14, fair)
+        r.set_option(15, a.grab)
+        y0, stride, rows = row_shard(H, n, 0)
+        out = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda")
+        r.trace_tile(u, make_ext(spp, bl, ml, frame=99), 0, y0, W, rows, y_stride=stride, out=out)
+        for f in range(a.frames):
+            ts.zero_()
+            r.set_wave_timeline(ts)
+            r.trace_tile(u, make_ext(spp, bl, ml, frame=f), 0, y0, W, rows, y_stride=stride, out=out)
+            torch.cuda.synchronize()
+            r.set_wave_timeline(None)
+            t = ts.cpu().numpy()
+            t = t[t[:, 2] > 0]
+            t0 = t[:, 0].min()
+            ent, stg, ext, ch = ((t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0, t[:, 3])
+            span = ext.max()
+            busy = (ext - np.maximum(stg, ent)).sum()
+            print(f"fair={fair} N={n} f{f}: waves {len(t)} span {span:8.1f}  entry p50/max {np.median(ent):6.1f}/{ent.max():6.1f}  "
+                  f"staged p50/max {np.median(stg):6.1f}/{stg.max():6.1f}  exit min/p10/p50/p90/max "
+                  f"{ext.min():7.1f}/{np.percentile(ext, 10):7.1f}/{np.median(ext):7.1f}/{np.percentile(ext, 90):7.1f}/"
+                  f"{ext.max():7.1f}  tail {span - ext.min():6.1f} ({(span - ext.min()) / span:.1%})  "
+                  f"chunks/wave {ch.mean():.2f} [{ch.min()}-{ch.max()}]  wave-busy {busy / (len(t) * span):.1%}",
+                  flush=True)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -66,18 +66,19 @@ def _worker_pipelined(rank, world, port, H, W, q):
     o = Oracle.from_scene(s)
     u = default_uniform(W, H, 0)
     y0, stride, rows = row_shard(H, world, rank)
-    g = FrameGatherer((rows_max(H, world), W, 4), H, "cpu")
-    frames = []
+    frames = {}
+    g = FrameGatherer((rows_max(H, world), W, 4), H, "cpu",
+                      on_frame=lambda k, fr: frames.__setitem__(k, fr.numpy().copy()))
     for f in range(3):
         t = g.tile().numpy()
         o.trace_tile(u, make_ext(2, 3, 15, frame=f), 0, y0, W, rows, y_stride=stride, out=t[:rows])
         g.put()
-        if rank == 0 and f >= 1:
-            frames.append(g.out.numpy().copy())  # frame f-1 is complete once frame f was put
+        if rank == 0:
+            assert sorted(frames) == list(range(max(0, f - 1)))  # frame k completes when its slot is reused
     out = g.flush()
     if rank == 0:
-        frames.append(out.numpy().copy())
-        q.put(np.stack(frames))
+        assert sorted(frames) == [0, 1, 2] and np.array_equal(out.numpy(), frames[2])
+        q.put(np.stack([frames[k] for k in range(3)]))
     dist.barrier()
     dist.destroy_process_group()
 

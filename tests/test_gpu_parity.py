@@ -134,6 +134,13 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "regtop-split2kb-b512-w6": (1, {1: 1, 3: 2, 7: 3, 9: 2, 2: 512, 5: 6}),
     "wavepersist-split20kb-b512-w6": (1, {1: 1, 3: 2, 9: 20, 2: 512, 5: 6}),
     "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
+    "leafinterior-ldsrects": (1, {1: 1, 3: 2, 7: 5, 8: 1}),
+    "ifif-ldsrects": (1, {1: 1, 3: 2, 7: 0, 8: 1}),
+    "leafinterior-grab3-fair": (1, {1: 1, 3: 2, 7: 5, 15: 3, 14: 1}),
+    "leafinterior-lds": (1, {1: 1, 3: 2, 7: 5, 8: 0, 11: 0}),
+    "leafinterior-split2kb": (1, {1: 1, 3: 2, 7: 5, 9: 2}),
+    "leafinterior-global": (1, {1: 0, 3: 2, 7: 5}),
+    "wavepersist-ldsrects-nofuse": (1, {1: 1, 3: 2, 8: 1, 12: 0}),
     "wavefront": (2, {}),
     "wavefront-global": (2, {1: 0}),
 }
@@ -171,7 +178,9 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
 
 
 @pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
-                                  "lean-ldsrects", "bouncerefill-ldsrects"])
+                                  "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
+                                  "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
+                                  "leafinterior-grab3-fair"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -247,10 +256,12 @@ def test_c4_eight_way_row_split_invariance(ren, gpu):
     assert rays == st.rays and st.paths == W * H * 16
 
 
-def test_accumulate_flag(ren, gpu):
+@pytest.mark.parametrize("fuse", [1, 0])
+def test_accumulate_flag(ren, gpu, fuse):
     from mirror_maze import MM_EXT_ACCUMULATE, default_uniform, make_ext
 
     ren.upload_scene(_scene(10))
+    ren.set_option(12, fuse)
     u = default_uniform(128, 96, 0)
     a, _ = ren.trace_tile(u, make_ext(4, 3, 15, frame=0), 0, 0, 128, 96)
     b, _ = ren.trace_tile(u, make_ext(4, 3, 15, frame=1), 0, 0, 128, 96)
@@ -284,8 +295,9 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}],
-                         ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects"])
+@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}],
+                         ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects",
+                              "leafinterior", "ifif"])
 def test_large_scene_top_of_tree_cache(gpu, opts):
     """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
     default kernel caches the top of the breadth-first node array in LDS and
