@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--contexts", type=int, default=0,
                    help="renderer contexts (one stream each) that consecutive frames alternate over; "
                         "0 = 1 on one GPU, 2 when the frame is split over ranks")
+    p.add_argument("--emulate-ranks", type=int, default=0,
+                   help="diagnostics on one GPU: trace only rank 0's row set of an N-rank split")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (approx)")
     return p.parse_args()
@@ -103,13 +105,16 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
 
 def main():
     args = parse()
+    # Exactly one JSON line on stdout: anything else written to fd 1 (e.g. the
+    # RCCL banner at communicator init) is sent to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from mirror_maze import MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, Renderer, Scene
     from mirror_maze import default_uniform, make_ext
-    from mirror_maze._lib import MM_OPT_TAIL_GATE
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -125,18 +130,19 @@ def main():
 
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[args.config]
     scene = Scene.build(maze_n, 0)
-    # Frames alternate over `contexts` renderer contexts, each on its own
-    # library stream: frames are independent, so frame k+1's blocks fill the
-    # CUs that frame k's last waves leave idle (the per-frame tail that bounds
-    # strong scaling: profiles/r01_scaling_probe.txt).
-    n_ctx = args.contexts if args.contexts > 0 else (1 if world == 1 else 2)
+    # Frames can alternate over two renderer contexts, each on its own library
+    # stream: frames are independent, so frame k+1's blocks fill the CUs that
+    # frame k's last waves leave idle -- the ~0.4 ms per-launch tail that
+    # bounds strong scaling (profiles/r01_timeline_probe.txt).  Two frames
+    # sharing the GPU also run ~7 % slower (profiles/r01_overlap_probe.txt), so
+    # overlap only pays on short per-rank frames: --contexts 0 (default)
+    # measures both issue modes after warmup and keeps the faster.
+    n_ctx = args.contexts if args.contexts > 0 else 2
     rens = []
     for _ in range(n_ctx):
         r = Renderer(local)
         r.set_pipeline({"auto": MM_PIPE_AUTO, "mega": MM_PIPE_MEGAKERNEL, "wave": MM_PIPE_WAVEFRONT}[args.pipeline])
         r.upload_scene(scene)
-        if n_ctx > 1:
-            r.set_option(MM_OPT_TAIL_GATE, 1)
         rens.append(r)
     streams = [r.own_stream() for r in rens]
     u = default_uniform(W, H, 0)
@@ -145,6 +151,8 @@ def main():
     from mirror_maze.dist import FrameGatherer, row_shard, rows_max
 
     y0, y_stride, my_rows = row_shard(H, world, rank)
+    if args.emulate_ranks > 1 and world == 1:
+        y0, y_stride, my_rows = row_shard(H, args.emulate_ranks, 0)
     frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     # one RCCL gather per frame, issued async on the frame's stream into
     # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
@@ -153,9 +161,10 @@ def main():
                 if distributed else None)
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in rens]
     last = [0]
+    active = [len(rens)]  # contexts the frames alternate over
 
     def step(k, frame, stats=False):
-        slot = k % len(rens)
+        slot = k % active[0]
         with torch.cuda.stream(streams[slot]):
             tile = gatherer.tile() if gatherer else tiles1[slot]
             _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
@@ -175,7 +184,25 @@ def main():
     for i in range(args.warmup):
         step(i, 10_000 + i)
     drain()
-    for r in rens:
+    calib = None
+    if args.contexts == 0:
+        calib = {}
+        for rep in range(2):
+            for m in (1, 2):
+                active[0] = m
+                if distributed:
+                    dist.barrier()
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for i in range(6):
+                    step(i, 20_000 + 8 * rep + i)
+                drain()
+                dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+                if distributed:
+                    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+                calib[m] = min(calib.get(m, 1e9), float(dt.item()) / 6 * 1e3)
+        active[0] = 2 if calib[2] < 0.98 * calib[1] else 1  # overlap only for a clear gain
+    for r in rens[:active[0]]:
         r.set_profiling(True)
         r.kernel_timing(reset=True)
     if distributed:
@@ -192,7 +219,7 @@ def main():
     elapsed = time.perf_counter() - t0
     drain()
     k_ms = k_launches = 0
-    for r in rens:
+    for r in rens[:active[0]]:
         ms, n = r.kernel_timing(reset=True)
         r.set_profiling(False)
         k_ms += ms
@@ -242,8 +269,11 @@ def main():
             "data": "synthetic: Kruskal maze seed 0 (host C++ restatement), default camera, RNG keyed (pixel,sample,frame)",
             "config": {"workload": desc, "maze_n": maze_n, "width": W, "height": H, "spp": spp,
                        "bounce_limit": bl, "mirror_limit": ml, "pipeline": args.pipeline,
-                       "parallelism": f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU",
-                       "frame_contexts": len(rens),
+                       "parallelism": (f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU") +
+                                      (f" (emulating rank 0 of {args.emulate_ranks})" if args.emulate_ranks > 1 else ""),
+                       "frame_contexts": active[0],
+                       "frame_contexts_calibration_ms": ({str(k): round(v, 3) for k, v in calib.items()}
+                                                         if calib else None),
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),
                        "node_visits_per_ray": round(visits_all / max(rays_all, 1), 2),
                        "rect_tests_per_ray": round(rtests_all / max(rays_all, 1), 2)},
@@ -251,8 +281,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "trace", "kernel_avg_ms": round(k_avg_s * 1e3, 3), "launches": k_launches,
                          "timing": ("HIP events around each launch on its stream" +
-                                    (f"; {len(rens)} contexts: consecutive launches overlap, so a launch's "
-                                     "span includes time shared with its neighbours" if len(rens) > 1 else "")),
+                                    ("; 2 contexts: consecutive launches overlap, so a launch's "
+                                     "span includes time shared with its neighbours" if active[0] > 1 else "")),
                          "bytes_per_ray": BYTES_PER_RAY,
                          "valu": {"achieved_tops": round(valu_ops / k_avg_s / 1e12, 3), "peak_tops": VALU_PEAK_TOPS,
                                   "frac": round(valu_ops / k_avg_s / 1e12 / VALU_PEAK_TOPS, 4),
@@ -261,7 +291,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene, u, make_ext(spp, bl, ml, frame=0), W, H, args.cpu_seconds)
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     for r in rens:
         r.close()
     if distributed:

@@ -626,6 +626,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
             const uint32_t block = c->opt_block ? c->opt_block : 1024u;
             const bool inst = (block == 256 && c->opt_min_waves == 8) || (block == 512 && c->opt_min_waves >= 6) ||
+                              (block == 768 && c->opt_min_waves == 6) ||
                               (block == 1024 && (c->opt_min_waves == 1 || c->opt_min_waves == 8));
             if (!inst)
                 return fail(c, MM_ERR_UNSUPPORTED, "wave-persistent kernel: block/min-waves pair not instantiated "
@@ -635,14 +636,17 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const int ww = c->opt_ww >= 0 ? c->opt_ww
                                           : ((block == 1024 && c->opt_min_waves == 8 && !c->opt_cold_lds) ? 5 : 0);
             const uint32_t slots = std::max(1u, c->depth);
-            // keep 2 blocks of 1024 (or their equivalent) resident: <= 80 KB of LDS per block
+            // LDS per block that keeps the launch-bound occupancy (min_waves per SIMD, 4 SIMDs):
+            // 1024/8 and 768/6 -> 2 blocks per CU -> 80 KB each
+            const size_t lds_budget = std::min<size_t>(160 * 1024, (size_t)(160 * 1024) * block /
+                                                                       (std::max(1u, c->opt_min_waves) * 256u));
             const size_t lds_total = 2 * (size_t)c->n_nodes * sizeof(float4) + (size_t)slots * block * 2;
-            const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= (size_t)(160 * 1024) * block / 2048;
+            const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= lds_budget;
             const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
-            const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * block / 2048;
+            const bool rects_fit = c->opt_lds_rects && lds_rects <= lds_budget;
             int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && ww != 4 ? 2 : 1)) : 0;
             const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
-            if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= (size_t)(160 * 1024) * block / 2048)
+            if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= lds_budget)
                 mode = 5;
             if (mode == 1 && (ww == 0 || ww == 5) && c->opt_glob_rects == 1) mode = 7;
             DevScene sc = dev_scene(c);
@@ -650,7 +654,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
                 // nodes exceed the LDS budget (or an explicit cache size is set):
                 // cache the top of the breadth-first array
-                const size_t budget = c->opt_lds_split == 1 ? (size_t)(160 * 1024) * block / 2048
+                const size_t budget = c->opt_lds_split == 1 ? lds_budget
                                                             : (size_t)c->opt_lds_split * 1024;
                 sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
                 mode = ((ww == 0 || ww == 5) && c->opt_glob_rects != 0) ? 6 : 4;

@@ -197,6 +197,9 @@ struct SplitNodes {
 __device__ __forceinline__ void node_pair(const float4* n, uint32_t lf, float4& la, float4& lb, float4& ra,
                                           float4& rb) {
     la = n[2 * lf]; lb = n[2 * lf + 1]; ra = n[2 * lf + 2]; rb = n[2 * lf + 3];
+#ifdef MM_FORCE_B128
+    asm volatile("" ::"v"(lb.w), "v"(rb.w));  // experiment: 16-B reads instead of 12-B (ds_read_b96)
+#endif
 }
 __device__ __forceinline__ void node_pair(const SplitNodes& n, uint32_t lf, float4& la, float4& lb, float4& ra,
                                           float4& rb) {
