@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--contexts", type=int, default=0,
                    help="renderer contexts (one stream each) that consecutive frames alternate over; "
                         "0 = 1 on one GPU, 2 when the frame is split over ranks")
+    p.add_argument("--accumulate", action="store_true",
+                   help="temporal accumulation (C5): every frame adds into one running sum per rank "
+                        "(MM_EXT_ACCUMULATE) and the frame is gathered once, after the last step")
     p.add_argument("--emulate-ranks", type=int, default=0,
                    help="diagnostics on one GPU: trace only rank 0's row set of an N-rank split")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -114,7 +117,7 @@ def main():
     import torch.distributed as dist
 
     from mirror_maze import MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, Renderer, Scene
-    from mirror_maze import default_uniform, make_ext
+    from mirror_maze import MM_EXT_ACCUMULATE, default_uniform, make_ext
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -137,7 +140,7 @@ def main():
     # sharing the GPU also run ~7 % slower (profiles/r01_overlap_probe.txt), so
     # overlap only pays on short per-rank frames: --contexts 0 (default)
     # measures both issue modes after warmup and keeps the faster.
-    n_ctx = args.contexts if args.contexts > 0 else 2
+    n_ctx = 1 if args.accumulate else (args.contexts if args.contexts > 0 else 2)
     rens = []
     for _ in range(n_ctx):
         r = Renderer(local)
@@ -163,9 +166,17 @@ def main():
     last = [0]
     active = [len(rens)]  # contexts the frames alternate over
 
+    acc_tile = (torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev)
+                if args.accumulate else None)
+
     def step(k, frame, stats=False):
         slot = k % active[0]
         with torch.cuda.stream(streams[slot]):
+            if acc_tile is not None:  # running sum of per-frame means; gathered once by drain()
+                _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame, flags=MM_EXT_ACCUMULATE),
+                                              0, y0, W, my_rows, y_stride=y_stride, out=acc_tile[:my_rows],
+                                              stats=stats)
+                return st
             tile = gatherer.tile() if gatherer else tiles1[slot]
             _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
                                           y_stride=y_stride, out=tile[:my_rows], stats=stats)
@@ -174,7 +185,19 @@ def main():
         last[0] = slot
         return st
 
+    def gather_accumulated():
+        with torch.cuda.stream(streams[0]):
+            if gatherer:
+                gatherer.tile().copy_(acc_tile)
+                gatherer.put()
+                gatherer.flush()
+            else:
+                tiles1[0].copy_(acc_tile[:H])
+                last[0] = 0
+
     def drain():
+        if acc_tile is not None:
+            gather_accumulated()
         if gatherer:
             gatherer.flush()
         torch.cuda.synchronize(dev)
@@ -185,7 +208,7 @@ def main():
         step(i, 10_000 + i)
     drain()
     calib = None
-    if args.contexts == 0:
+    if args.contexts == 0 and not args.accumulate:
         calib = {}
         for rep in range(2):
             for m in (1, 2):
@@ -209,8 +232,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if acc_tile is not None:
+        with torch.cuda.stream(streams[0]):
+            acc_tile.zero_()
     for i in range(args.steps):
         step(i, i)
+    if acc_tile is not None:
+        gather_accumulated()  # C5: one gather of the accumulated frame, inside the timed region
     if gatherer:
         gatherer.flush()  # the last frames' gathers + assembly are inside the timed region
     torch.cuda.synchronize(dev)
@@ -272,6 +300,7 @@ def main():
                        "parallelism": (f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU") +
                                       (f" (emulating rank 0 of {args.emulate_ranks})" if args.emulate_ranks > 1 else ""),
                        "frame_contexts": active[0],
+                       "temporal_accumulation": bool(args.accumulate),
                        "frame_contexts_calibration_ms": ({str(k): round(v, 3) for k, v in calib.items()}
                                                          if calib else None),
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),

@@ -333,8 +333,8 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_LDS_STACK: c->opt_lds_stack = value != 0; return MM_OK;
         case MM_OPT_TRAVERSAL:
             if (value != -1 && value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 5 &&
-                value != 8 && value != 16 && value != 32)
-                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0, 1, 2, 3, 4, 5, 8, 16 or 32");
+                value != 6 && value != 8 && value != 16 && value != 32)
+                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0-6, 8, 16 or 32");
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
@@ -567,15 +567,17 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: tile outside the frame");
     HIPC(c, hipSetDevice(c->device));
     const bool want_stats = (e->flags & MM_EXT_COUNT_STATS) != 0;
-    // Bound the per-sample staging buffer: process whole rows, <= 64 Mi paths.
+    // Bound the per-sample staging buffer: process whole rows, <= 64 Mi paths
+    // (32 Mi in the wavefront pipeline).  With the fused resolve there is no
+    // staging buffer: one launch covers up to 2^31 paths (a whole C5 frame).
     const uint64_t row_paths = (uint64_t)w * e->spp;
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
-    const uint64_t batch_paths = wave ? (32ull << 20) : (64ull << 20);
+    // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
+    const bool fuse = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_ww != 4 && c->opt_ww != 6 &&
+                      c->opt_fuse && 64 % e->spp == 0;
+    const uint64_t batch_paths = fuse ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
-    // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
-    const bool fuse = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_ww != 4 &&
-                      c->opt_fuse && 64 % e->spp == 0;
     int rc = fuse ? MM_OK : ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
     if (rc) return rc;
     // aux: [0..3] stats (zeroed only when counted), [4] sticky error flag
@@ -644,13 +646,13 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= lds_budget;
             const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
             const bool rects_fit = c->opt_lds_rects && lds_rects <= lds_budget;
-            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && ww != 4 ? 2 : 1)) : 0;
+            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && ww != 4 && ww != 6 ? 2 : 1)) : 0;
             const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
             if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= lds_budget)
                 mode = 5;
             if (mode == 1 && (ww == 0 || ww == 5) && c->opt_glob_rects == 1) mode = 7;
             DevScene sc = dev_scene(c);
-            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5) &&
+            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
                 // nodes exceed the LDS budget (or an explicit cache size is set):
                 // cache the top of the breadth-first array

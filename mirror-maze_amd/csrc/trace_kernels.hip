@@ -249,7 +249,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
 // boundary instead of idling until the wave's longest path ends.  The wave
 // runs one bounce (closest hit + shade) per iteration for all lanes; every
 // path's operation sequence is trace_path's, so samples are bit-identical.
-template <bool kStats, typename V, typename Stack, typename Cold = NoCold>
+template <bool kStats, typename V, typename Stack, int kTrav = 0, typename Cold = NoCold>
 __device__ __forceinline__ uint32_t bouncerefill_body(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
                                                   float4* __restrict__ samples, unsigned long long* stats,
                                                   uint32_t* err, uint32_t* work) {
@@ -310,7 +310,7 @@ __device__ __forceinline__ uint32_t bouncerefill_body(const DevScene& sc, const 
             if (!fin) {  // one bounce: shaders.metal:306-340
                 float t = kBig;
                 uint32_t k = 0;
-                const bool ok = closest_hit<kStats, V, Stack, 0>(sc, v, p.ori, p.dir, t, k, stack, c);
+                const bool ok = closest_hit<kStats, V, Stack, kTrav>(sc, v, p.ori, p.dir, t, k, stack, c);
                 if (kStats) c.rays++;
                 if (!ok) atomicOr(err, 1u);
                 fin = !ok || !shade_step(sc, p, t, k, mirror_limit);
@@ -334,6 +334,7 @@ __device__ __forceinline__ uint32_t wp_dispatch(const DevScene& sc, const V& v, 
                                                 float4* __restrict__ samples, unsigned long long* stats,
                                                 uint32_t* err, uint32_t* work, const Cold& cold = Cold{}) {
     if constexpr (kWW == 4) return bouncerefill_body<kStats>(sc, v, stack, job, samples, stats, err, work);
+    else if constexpr (kWW == 6) return bouncerefill_body<kStats, V, Stack, 5>(sc, v, stack, job, samples, stats, err, work);
     else return wavepersist_body<kStats, kWW>(sc, v, stack, job, samples, stats, err, work, cold);
 }
 
@@ -478,6 +479,7 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
     if (block == 1024 && min_waves == 8 && loop_form == 5) {
         MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP3(1024, 8, 5)
     }
+    if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
     // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS
     if (block == 768 && min_waves == 6 && loop_form == 5) { MM_WP2(3, 768, 6, 5) MM_WP2(6, 768, 6, 5) }
 #undef MM_WP

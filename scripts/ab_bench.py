@@ -66,6 +66,7 @@ for _f in (1,):
 for _g in (2, 4, 8):
     VARIANTS[f"grab{_g}"] = dict(pipe=1, grab=_g)
 VARIANTS["li-b768-w6"] = dict(pipe=1, persist=2, lds=1, block=768, mw=6, ls=0, lr=1, ww=5)
+VARIANTS["brli-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=6)
 VARIANTS["li-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=5)
 VARIANTS["li-lds"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, ww=5)
 VARIANTS["li-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=5)

@@ -221,6 +221,98 @@ void lockstep(const std::vector<const uint8_t*>& lanes, int mode, const Cost& c,
 
 }  // namespace
 
+// Path -> lane mappings of a 64-path chunk over a band of 8 rows (spp = 8):
+// 0 current (8 consecutive pixels of a row x 8 samples), 1 2x4 pixel tile x 8
+// samples, 2 4x2 tile x 8, 3 8x8 pixel tile x 1 sample (sample s of the tile
+// in chunk s), 4 64 consecutive pixels of a row x 1 sample.
+int map_mode(const Scene& sc, const mm_uniform& u, V3 cam, uint32_t W, uint32_t H, uint32_t spp, int bl, int ml,
+             uint32_t band_step) {
+    if (spp != 8) { fprintf(stderr, "mapping study needs spp 8\n"); return 1; }
+    const int NM = 5;
+    const char* names[NM] = {"8 px (row) x 8 spp  [current]", "2x4 px tile x 8 spp", "4x2 px tile x 8 spp",
+                             "8x8 px tile x 1 spp", "64 px (row) x 1 spp"};
+    std::vector<double> valu(NM, 0.0), iters(NM, 0.0);
+    std::vector<uint32_t> bands;
+    for (uint32_t y = 0; y + 8 <= H; y += band_step) bands.push_back(y);
+    Cost c;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (size_t bi = 0; bi < bands.size(); ++bi) {
+        const uint32_t y0 = bands[bi];
+        std::vector<uint8_t> buf;
+        std::vector<std::vector<uint32_t>> prays((size_t)8 * W * spp);
+        auto pid = [&](uint32_t px, uint32_t dy, uint32_t s) { return ((size_t)dy * W + px) * spp + s; };
+        for (uint32_t dy = 0; dy < 8; ++dy)
+            for (uint32_t px = 0; px < W; ++px)
+                for (uint32_t s = 0; s < spp; ++s) {
+                    const uint32_t y = y0 + dy;
+                    uint32_t seed = seed_tile(y * W + px, s, g_frame);
+                    V3 d = primary(u, px, y);
+                    float j1 = rand_pm1(seed), j2 = rand_pm1(seed);
+                    d = d + V3{j1 * 0.001f, j2 * 0.001f, 0.0f * 0.001f};
+                    std::vector<uint32_t> keys;
+                    trace(sc, cam, d, seed, bl, ml, buf, prays[pid(px, dy, s)], keys);
+                }
+        std::vector<double> lv(NM, 0.0), li(NM, 0.0);
+        for (int m = 0; m < NM; ++m) {
+            std::vector<std::vector<size_t>> chunks;
+            if (m == 0) {
+                for (uint32_t dy = 0; dy < 8; ++dy)
+                    for (uint32_t px = 0; px < W; px += 8) {
+                        std::vector<size_t> ch;
+                        for (uint32_t k = 0; k < 8; ++k) for (uint32_t s = 0; s < 8; ++s) ch.push_back(pid(px + k, dy, s));
+                        chunks.push_back(ch);
+                    }
+            } else if (m == 1 || m == 2) {
+                const uint32_t tw = m == 1 ? 4 : 2, th = m == 1 ? 2 : 4;
+                for (uint32_t dy = 0; dy < 8; dy += th)
+                    for (uint32_t px = 0; px < W; px += tw) {
+                        std::vector<size_t> ch;
+                        for (uint32_t j = 0; j < th; ++j) for (uint32_t i = 0; i < tw; ++i)
+                            for (uint32_t s = 0; s < 8; ++s) ch.push_back(pid(px + i, dy + j, s));
+                        chunks.push_back(ch);
+                    }
+            } else if (m == 3) {
+                for (uint32_t px = 0; px < W; px += 8)
+                    for (uint32_t s = 0; s < 8; ++s) {
+                        std::vector<size_t> ch;
+                        for (uint32_t j = 0; j < 8; ++j) for (uint32_t i = 0; i < 8; ++i) ch.push_back(pid(px + i, j, s));
+                        chunks.push_back(ch);
+                    }
+            } else {
+                for (uint32_t dy = 0; dy < 8; ++dy)
+                    for (uint32_t px = 0; px < W; px += 64)
+                        for (uint32_t s = 0; s < 8; ++s) {
+                            std::vector<size_t> ch;
+                            for (uint32_t i = 0; i < 64 && px + i < W; ++i) ch.push_back(pid(px + i, dy, s));
+                            chunks.push_back(ch);
+                        }
+            }
+            Tally t;
+            for (auto& ch : chunks) {
+                size_t maxb = 0;
+                for (size_t q : ch) maxb = std::max(maxb, prays[q].size());
+                for (size_t b = 0; b < maxb; ++b) {
+                    std::vector<const uint8_t*> lanes(64, nullptr);
+                    for (size_t l = 0; l < ch.size(); ++l)
+                        if (b < prays[ch[l]].size()) lanes[l] = &buf[prays[ch[l]][b]];
+                    t.valu += c.shade;
+                    lockstep(lanes, 1, c, t);
+                }
+                t.valu += c.setup;
+            }
+            lv[m] = t.valu;
+            li[m] = t.iters;
+        }
+#pragma omp critical
+        for (int m = 0; m < NM; ++m) { valu[m] += lv[m]; iters[m] += li[m]; }
+    }
+    printf("# path->lane mappings, loop form 5 lockstep model, %zu bands of 8 rows (every %u rows)\n", bands.size(),
+           band_step);
+    for (int m = 0; m < NM; ++m)
+        printf("%-34s iters %10.0f  VALU(model) %12.4g  rel %.3f\n", names[m], iters[m], valu[m], valu[m] / valu[0]);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     uint32_t N = argc > 1 ? atoi(argv[1]) : 32, W = argc > 2 ? atoi(argv[2]) : 1920, H = argc > 3 ? atoi(argv[3]) : 1080;
     uint32_t spp = argc > 4 ? atoi(argv[4]) : 8;
@@ -233,6 +325,7 @@ int main(int argc, char** argv) {
     mm_uniform u;
     mm_uniform_default((float)W, (float)H, 0, &u);
     const V3 cam = {u.cam.center[0], u.cam.center[1], u.cam.center[2]};
+    if (getenv("MAPS")) return map_mode(sc, u, cam, W, H, spp, bl, ml, row_step);
 
     // rows sampled: y = 0, row_step, ...; a "chunk" is 64 consecutive paths of
     // one row (path = pixel*spp + sample, as the kernel numbers them)
