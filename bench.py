@@ -290,6 +290,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "samples_per_s": round(paths_all / elapsed, 1),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
