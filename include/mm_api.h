@@ -138,7 +138,8 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   -1 auto: 5 at 1024 threads / 8 waves, else 0 (default)
                                   8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
 #define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
-#define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 0 scratch (default) */
+#define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 2 the same
+                                  with the compact rect records through L1/L2 (loop form 5), 0 scratch (default) */
 #define MM_OPT_LDS_SPLIT   9   /* wave-persistent kernel, BVH larger than the LDS budget: cache the top of
                                   the (breadth-first) node array in LDS, rest via L1/L2.
                                   0 off, 1 auto size (default), >1: always use a cache of this many KB */
@@ -156,6 +157,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   mean chunk count (evens out per-wave progress), 0 default */
 #define MM_OPT_GRAB       15  /* wave-persistent kernel: 64-path chunks a wave claims per atomic on the
                                   work counter, 1..16 (1 default) */
+#define MM_OPT_BLOCKSYNC  16  /* 1: block-synchronous bounces, the live rays of each 1024-path block
+                                  compacted before every closest-hit pass (experimental; nodes must
+                                  fit 47 KB of LDS beside the 32 KB exchange), 0 default */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

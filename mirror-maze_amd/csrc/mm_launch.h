@@ -56,6 +56,12 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
                                     int loop_form, hipStream_t s);
 
+// Throughput mode, block-synchronous bounces with ray compaction
+// (trace_block.hip, MM_OPT_BLOCKSYNC): 1024-thread blocks, BVH in LDS.
+size_t blocksync_lds_bytes(const DevScene& sc, uint32_t block);
+hipError_t launch_trace_blocksync(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
+                                  uint32_t* err, uint32_t* work, bool count_stats, hipStream_t s);
+
 struct PersistOpts {
     int lds_mode = 1;          // 0 nodes via cache, 1 nodes in LDS, 3 nodes + compact rects in LDS
     uint32_t block = 1024;

@@ -80,14 +80,15 @@ struct mm_ctx {
     int opt_ww = -1;             // traversal loop: -1 auto (5 at 1024/8, else 0), 0 if-if, 1 while-while,
                                  // 5 leaf+interior per iteration, 8/16/32 leaf batch
     int opt_lds_rects = 1;       // compact rect records in LDS next to the BVH when they fit
-    int opt_lds_stack = 0;       // u16 LDS stack: measured equal to scratch (profiles/r01_ab_ldsstack.txt)
+    int opt_lds_stack = 0;       // u16 LDS stack: 1 with LDS nodes only, 2 + rect records via L1/L2 (form 5)
     uint32_t opt_threshold = 32;
-    bool opt_fuse = true;
-    bool opt_tail_gate = false;
-    uint32_t opt_fair = 0;       // MM_OPT_FAIR bits
+    bool opt_fuse = true;        // resolve fused into the wave-persistent kernel when 64 % spp == 0
+    bool opt_tail_gate = false;  // one-wave no-op ahead of each trace launch (contexts sharing the GPU)
+    uint32_t opt_fair = 0;       // MM_OPT_FAIR: issue priority for waves behind the mean chunk count
     uint32_t opt_grab = 1;       // chunks per work-counter atomic
+    bool opt_blocksync = false;  // block-synchronous bounces with ray compaction (trace_block.hip)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
-    uint32_t wave_ts_cap = 0;  // one-wave no-op ahead of each trace launch (contexts sharing the GPU)        // resolve fused into the wave-persistent kernel when 64 % spp == 0
+    uint32_t wave_ts_cap = 0;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
@@ -330,7 +331,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "threshold must be 0..63");
             c->opt_threshold = (uint32_t)value;
             return MM_OK;
-        case MM_OPT_LDS_STACK: c->opt_lds_stack = value != 0; return MM_OK;
+        case MM_OPT_LDS_STACK:
+            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "lds stack must be 0, 1 or 2");
+            c->opt_lds_stack = value;
+            return MM_OK;
         case MM_OPT_TRAVERSAL:
             if (value != -1 && value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 5 &&
                 value != 6 && value != 8 && value != 16 && value != 32)
@@ -340,6 +344,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
         case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
+        case MM_OPT_BLOCKSYNC: c->opt_blocksync = value != 0; return MM_OK;
         case MM_OPT_GRAB:
             if (value < 1 || value > 16) return fail(c, MM_ERR_INVALID, "grab must be 1..16");
             c->opt_grab = (uint32_t)value;
@@ -625,6 +630,11 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                 launches += 2;
             }
             launches += 1;
+        } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_blocksync &&
+                   blocksync_lds_bytes(dev_scene(c), 1024) <= 80 * 1024) {
+            HIPC(c, launch_trace_blocksync(dev_scene(c), job, c->d_samples, c->d_aux,
+                                           reinterpret_cast<uint32_t*>(c->d_aux + 4),
+                                           reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, c->stream));
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
             const uint32_t block = c->opt_block ? c->opt_block : 1024u;
             const bool inst = (block == 256 && c->opt_min_waves == 8) || (block == 512 && c->opt_min_waves >= 6) ||
@@ -651,6 +661,10 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= lds_budget)
                 mode = 5;
             if (mode == 1 && (ww == 0 || ww == 5) && c->opt_glob_rects == 1) mode = 7;
+            // LDS stack beside the nodes, compact rect records through L1/L2 (loop form 5)
+            if (lds_fits && ww == 5 && c->opt_lds_stack == 2 && c->stack16_ok && block == 1024 &&
+                c->opt_min_waves == 8 && lds_total <= lds_budget)
+                mode = 8;
             DevScene sc = dev_scene(c);
             if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {

@@ -10,6 +10,7 @@
 
 #include "mm_launch.h"
 #include "mm_trace.h"
+#include "mm_wave_util.h"
 
 namespace mm {
 
@@ -33,23 +34,6 @@ __global__ void k_prep_rects(const mm_rect* __restrict__ rects, uint32_t n, floa
 hipError_t launch_prep_rects(const mm_rect* rects_dev, uint32_t n, float4* geo_dev, hipStream_t s) {
     hipLaunchKernelGGL(k_prep_rects, dim3((n + 255) / 256), dim3(256), 0, s, rects_dev, n, geo_dev);
     return hipGetLastError();
-}
-
-// Sum per-thread counters over the wave, one atomic per wave.
-__device__ __forceinline__ void flush_stats(unsigned long long* stats, const Counters& c, uint32_t paths) {
-    unsigned long long v[4] = {c.rays, c.visits, c.rtests, paths};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        unsigned long long x = v[i];
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-        v[i] = x;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&stats[0], v[0]);
-        atomicAdd(&stats[1], v[1]);
-        atomicAdd(&stats[2], v[2]);
-        atomicAdd(&stats[3], v[3]);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -146,41 +130,6 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
         samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
     }
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
-}
-
-// The per-pixel reduction of k_resolve done inside a wave: with 64 % spp == 0
-// and chunks starting at multiples of 64, a wave's 64 paths are 64/spp whole
-// pixels (lanes [p*spp, (p+1)*spp)).  spp % 8 == 0: pairwise tree in blocks of
-// 8 by xor-shuffles (a+b == b+a exactly), blocks added left to right by the
-// pixel's first lane; otherwise a left-to-right sum.  Then / spp -- the same
-// operations in the same order as k_resolve, so the pixel is bit-identical.
-// Called by all 64 lanes (uniform control flow); `valid` lanes' pixels written.
-__device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32_t path, bool valid) {
-    const uint32_t spp = job.e.spp, lane = threadIdx.x & 63u;
-    F3 acc;
-    if (spp % 8 == 0) {
-        s = s + F3{__shfl_xor(s.x, 1), __shfl_xor(s.y, 1), __shfl_xor(s.z, 1)};
-        s = s + F3{__shfl_xor(s.x, 2), __shfl_xor(s.y, 2), __shfl_xor(s.z, 2)};
-        s = s + F3{__shfl_xor(s.x, 4), __shfl_xor(s.y, 4), __shfl_xor(s.z, 4)};
-        acc = s;
-        for (uint32_t b = 8; b < spp; b += 8)
-            acc = acc + F3{__shfl(s.x, (int)(lane + b)), __shfl(s.y, (int)(lane + b)), __shfl(s.z, (int)(lane + b))};
-    } else {
-        acc = s;
-        for (uint32_t k = 1; k < spp; ++k)
-            acc = acc + F3{__shfl(s.x, (int)(lane + k)), __shfl(s.y, (int)(lane + k)), __shfl(s.z, (int)(lane + k))};
-    }
-    if (valid && (lane & (spp - 1)) == 0) {
-        const uint32_t pix = path / spp;
-        const float m = (float)spp;
-        const F3 v = F3{acc.x / m, acc.y / m, acc.z / m};
-        if (job.e.flags & MM_EXT_ACCUMULATE) {
-            const float4 o = job.out[pix];
-            job.out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
-        } else {
-            job.out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
-        }
-    }
 }
 
 // Wave-persistent megakernel: resident blocks (LDS filled once per block);
@@ -347,7 +296,8 @@ template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, Scr
 // 3 nodes + compact rect records in LDS, 4 top of the tree in LDS (the first
 // sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2,
 // 5 nodes in LDS + each path's T and L parked in LDS while it traverses,
-// 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same.
+// 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same,
+// 8 = 2 + the same (nodes and u16 stack in LDS, rect records via L1/L2).
 // Diagnostics: time at which the block's LDS staging completed (wave timeline).
 #define MM_TS_STAGED()                                                                                      \
     do {                                                                                                     \
@@ -397,12 +347,15 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
             WpStack<kWW> st;
             const LdsCold cold{reinterpret_cast<float*>(lds_recs) + threadIdx.x, blockDim.x};
             chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work, cold);
-        } else if constexpr (kLds == 2) {
+        } else if constexpr (kLds == 2 || kLds == 8) {
             LdsStack16 st;
             st.base = reinterpret_cast<uint16_t*>(lds_recs) + threadIdx.x;
             st.stride = blockDim.x;
             st.cap = stack_slots;
-            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            if constexpr (kLds == 8)  // + compact rect records through L1/L2
+                chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, sc.recs), st, job, samples, stats, err, work);
+            else
+                chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
         } else {
             WpStack<kWW> st;
             chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
@@ -441,7 +394,7 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     const size_t lds = (kLds == 4 || kLds == 6) ? (size_t)sc.n_lds_f4 * sizeof(float4)
                                  : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
                                        (kLds == 5 ? 6 * (size_t)block * sizeof(float) : 0) +
-                                       (kLds == 2 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
+                                       (kLds == 2 || kLds == 8 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
                                        (kLds == 3 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves, kWW>
                             : k_trace_wavepersist<false, kLds, kBlock, kMinWaves, kWW>;
@@ -477,7 +430,7 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
         MM_WP3(B, W, 32) }
     MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
     if (block == 1024 && min_waves == 8 && loop_form == 5) {
-        MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP3(1024, 8, 5)
+        MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP2(8, 1024, 8, 5) MM_WP3(1024, 8, 5)
     }
     if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
     // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS

@@ -67,6 +67,10 @@ for _g in (2, 4, 8):
     VARIANTS[f"grab{_g}"] = dict(pipe=1, grab=_g)
 VARIANTS["li-b768-w6"] = dict(pipe=1, persist=2, lds=1, block=768, mw=6, ls=0, lr=1, ww=5)
 VARIANTS["brli-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=6)
+VARIANTS["blocksync"] = dict(pipe=1, bsync=1)
+VARIANTS["li-ldsstack-grec"] = dict(pipe=1, ls=2)
+VARIANTS["li-ldsstack"] = dict(pipe=1, ls=1, lr=0)
+VARIANTS["li-lds-grec"] = dict(pipe=1, lr=0, gr=1)
 VARIANTS["li-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=5)
 VARIANTS["li-lds"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=0, ww=5)
 VARIANTS["li-split1"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, split=1, ww=5)
@@ -114,6 +118,8 @@ def main():
             r.set_option(7, v["ww"])
         elif v.get("persist") == 2:
             r.set_option(7, 0)  # historical wp-* variants: the if-if loop
+        if "bsync" in v:
+            r.set_option(16, v["bsync"])
         if "grab" in v:
             r.set_option(15, v["grab"])
         if "fair" in v:

@@ -137,6 +137,8 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "leafinterior-ldsrects": (1, {1: 1, 3: 2, 7: 5, 8: 1}),
     "ifif-ldsrects": (1, {1: 1, 3: 2, 7: 0, 8: 1}),
     "leafinterior-grab3-fair": (1, {1: 1, 3: 2, 7: 5, 15: 3, 14: 1}),
+    "blocksync": (1, {3: 2, 16: 1}),
+    "blocksync-nofuse": (1, {3: 2, 16: 1, 12: 0}),
     "leafinterior-lds": (1, {1: 1, 3: 2, 7: 5, 8: 0, 11: 0}),
     "leafinterior-split2kb": (1, {1: 1, 3: 2, 7: 5, 9: 2}),
     "leafinterior-global": (1, {1: 0, 3: 2, 7: 5}),
@@ -180,7 +182,7 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
 @pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
                                   "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
                                   "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
-                                  "leafinterior-grab3-fair"])
+                                  "leafinterior-grab3-fair", "blocksync"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -320,3 +322,23 @@ def test_large_scene_top_of_tree_cache(gpu, opts):
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
         assert (st.rays, st.node_visits, st.rect_tests) == (rst.rays, rst.node_visits, rst.rect_tests)
     r.close()
+
+
+def test_bench_prints_one_json_line(gpu):
+    """bench.py's driver contract: exactly one JSON line on stdout with the
+    metric, the roofline and the issue-mode calibration (short C2 run)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--config", "c2", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["unit"] == "Mrays/s" and d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2
+    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    assert d["config"]["frame_contexts"] in (1, 2)
