@@ -61,6 +61,8 @@ def parse():
                         "(MM_EXT_ACCUMULATE) and the frame is gathered once, after the last step")
     p.add_argument("--emulate-ranks", type=int, default=0,
                    help="diagnostics on one GPU: trace only rank 0's row set of an N-rank split")
+    p.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                   help="mm_set_option on every context (MM_OPT_* numbers, include/mm_api.h); results never change")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (approx)")
     return p.parse_args()
@@ -146,6 +148,9 @@ def main():
         r = Renderer(local)
         r.set_pipeline({"auto": MM_PIPE_AUTO, "mega": MM_PIPE_MEGAKERNEL, "wave": MM_PIPE_WAVEFRONT}[args.pipeline])
         r.upload_scene(scene)
+        for kv in args.opt:
+            k, v = kv.split("=")
+            r.set_option(int(k), int(v))
         rens.append(r)
     streams = [r.own_stream() for r in rens]
     u = default_uniform(W, H, 0)
@@ -302,6 +307,7 @@ def main():
                                       (f" (emulating rank 0 of {args.emulate_ranks})" if args.emulate_ranks > 1 else ""),
                        "frame_contexts": active[0],
                        "temporal_accumulation": bool(args.accumulate),
+                       "options": args.opt or None,
                        "frame_contexts_calibration_ms": ({str(k): round(v, 3) for k, v in calib.items()}
                                                          if calib else None),
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),

@@ -139,7 +139,8 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
 #define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
 #define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 2 the same
-                                  with the compact rect records through L1/L2 (loop form 5), 0 scratch (default) */
+                                  with the compact rect records through L1/L2 (loop form 5), 3 u16 entries in
+                                  scratch (loop form 5), 0 u32 entries in scratch (default) */
 #define MM_OPT_LDS_SPLIT   9   /* wave-persistent kernel, BVH larger than the LDS budget: cache the top of
                                   the (breadth-first) node array in LDS, rest via L1/L2.
                                   0 off, 1 auto size (default), >1: always use a cache of this many KB */

@@ -15,6 +15,10 @@
  *                                                          src/maths.rs:139-156
  *   mm_chunks_*       chunk scheduler gen_pixels/random_pixels
  *                                                          src/main.rs:293-326
+ *   mm_player_*, mm_check_collision, mm_quat_mult, mm_update_quat_angle
+ *                     interactive camera + collision       src/main.rs:265-291,
+ *                                                          738-842, 922-924;
+ *                                                          src/maths.rs:159-178
  */
 #ifndef MM_SCENE_H
 #define MM_SCENE_H
@@ -102,6 +106,35 @@ int  mm_chunks_create(float view_w, float view_h, uint32_t chunk_w, uint64_t see
 uint32_t mm_chunks_total(const mm_chunk_sched* s);
 int  mm_chunks_next(mm_chunk_sched* s, uint32_t n, uint32_t* out_xy /* n*2 */);
 void mm_chunks_free(mm_chunk_sched* s);
+
+/* ---- interactive camera and player collision (src/main.rs:265-291, 738-842,
+ * 922-924; src/maths.rs:159-178) -- SURVEY.md §8f item 4.  Drives the camera of
+ * an offline sequence (or a front end) exactly as the reference's event loop.  */
+typedef struct mm_player {
+    float center[3];        /* camera_center, starts at (-5, 0, -45)          */
+    float quat[4];          /* rotation (x, y, z, w)                           */
+    float half_theta;       /* mouse-driven half angle, acos(quat.w) at start  */
+    float fps;              /* 60 (main.rs:760): a key moves 5/fps per frame   */
+} mm_player;
+#define MM_PLAYER_COLLIDED  0x1u   /* the move was undone (check_collision hit)   */
+#define MM_PLAYER_ROTATED   0x2u   /* quat changed: the reference regenerates its chunk list */
+#define MM_PLAYER_NAN_QUAT  0x4u   /* rotation rejected (reference prints "Help!") */
+/* v' = q^-1 (v, 0) q  (quat_mult, maths.rs:175-178) */
+void mm_quat_mult(const float v[3], const float q[4], float out[3]);
+/* same axis, half angle theta (update_quat_angle, maths.rs:159-162) */
+void mm_update_quat_angle(const float q[4], float theta, float out[4]);
+/* first leaf (node index) whose box overlaps [bmin, bmax] in the reference's
+ * recursive order (check_collision, main.rs:265-291); -1 none, -2 bad tree */
+int  mm_check_collision(const mm_node* nodes, uint32_t n_nodes, const float bmin[3], const float bmax[3]);
+int  mm_player_init(const float quat[4], mm_player* p);
+/* One frame: keys (macOS key codes 0 A, 1 S, 2 D, 13 W, in pressed order) move
+ * the camera, a collision with the player box (+-0.5, 0.2, 0.5) undoes the
+ * move, then the previous frame's mouse deltaX values turn half_theta and the
+ * quaternion.  *flags receives MM_PLAYER_* bits. */
+int  mm_player_step(mm_player* p, const uint16_t* keys, uint32_t n_keys, const float* mouse_dx, uint32_t n_mouse,
+                    const mm_node* nodes, uint32_t n_nodes, uint32_t* flags);
+/* mm_uniform_default with the player's camera centre and rotation. */
+int  mm_player_uniform(const mm_player* p, float view_w, float view_h, uint32_t time, mm_uniform* u);
 
 #ifdef __cplusplus
 }

@@ -80,7 +80,8 @@ struct mm_ctx {
     int opt_ww = -1;             // traversal loop: -1 auto (5 at 1024/8, else 0), 0 if-if, 1 while-while,
                                  // 5 leaf+interior per iteration, 8/16/32 leaf batch
     int opt_lds_rects = 1;       // compact rect records in LDS next to the BVH when they fit
-    int opt_lds_stack = 0;       // u16 LDS stack: 1 with LDS nodes only, 2 + rect records via L1/L2 (form 5)
+    int opt_lds_stack = 0;       // u16 stack: 1 in LDS with LDS nodes only, 2 + rect records via L1/L2 (form 5),
+                                 // 3 in scratch beside LDS nodes + records (form 5)
     uint32_t opt_threshold = 32;
     bool opt_fuse = true;        // resolve fused into the wave-persistent kernel when 64 % spp == 0
     bool opt_tail_gate = false;  // one-wave no-op ahead of each trace launch (contexts sharing the GPU)
@@ -332,7 +333,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_threshold = (uint32_t)value;
             return MM_OK;
         case MM_OPT_LDS_STACK:
-            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "lds stack must be 0, 1 or 2");
+            if (value < 0 || value > 3) return fail(c, MM_ERR_INVALID, "lds stack must be 0..3");
             c->opt_lds_stack = value;
             return MM_OK;
         case MM_OPT_TRAVERSAL:
@@ -665,6 +666,10 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             if (lds_fits && ww == 5 && c->opt_lds_stack == 2 && c->stack16_ok && block == 1024 &&
                 c->opt_min_waves == 8 && lds_total <= lds_budget)
                 mode = 8;
+            // u16 stack entries in scratch beside LDS nodes + records (loop form 5)
+            if (mode == 3 && ww == 5 && c->opt_lds_stack == 3 && c->stack16_ok && block == 1024 &&
+                c->opt_min_waves == 8)
+                mode = 9;
             DevScene sc = dev_scene(c);
             if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {

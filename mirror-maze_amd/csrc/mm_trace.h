@@ -130,6 +130,20 @@ struct ScratchStack {          // the reference's 50-entry private array
     __device__ __forceinline__ void push(uint32_t i, uint32_t v) { s[i] = v; }
     __device__ __forceinline__ uint32_t pop(uint32_t i) const { return s[i]; }
 };
+// The reference stack with u16 entries (count << 12 | left_first; needs
+// count < 16 and left_first < 4096, checked at upload): half the scratch
+// footprint, so the traversal stacks of all resident waves stay in L2.
+struct ScratchStack16 {
+    uint16_t s[kStackMax];
+    static constexpr uint32_t kCap = kStackMax;
+    __device__ __forceinline__ void push(uint32_t i, uint32_t v) {
+        s[i] = (uint16_t)(((v >> 24) << 12) | (v & 0xFFFu));
+    }
+    __device__ __forceinline__ uint32_t pop(uint32_t i) const {
+        const uint32_t p = s[i];
+        return ((p >> 12) << 24) | (p & 0xFFFu);
+    }
+};
 // The same stack with its top entry held in a register: a pop returns the
 // register and reloads the next entry from scratch, whose latency then
 // overlaps the following traversal step instead of stalling the next node

@@ -297,7 +297,8 @@ template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, Scr
 // sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2,
 // 5 nodes in LDS + each path's T and L parked in LDS while it traverses,
 // 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same,
-// 8 = 2 + the same (nodes and u16 stack in LDS, rect records via L1/L2).
+// 8 = 2 + the same (nodes and u16 stack in LDS, rect records via L1/L2),
+// 9 = 3 with u16 traversal-stack entries in scratch.
 // Diagnostics: time at which the block's LDS staging completed (wave timeline).
 #define MM_TS_STAGED()                                                                                      \
     do {                                                                                                     \
@@ -336,12 +337,15 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
         extern __shared__ float4 lds_nodes[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
         uint2* lds_recs = reinterpret_cast<uint2*>(lds_nodes + 2 * sc.n_nodes);
-        if constexpr (kLds == 3)
+        if constexpr (kLds == 3 || kLds == 9)
             for (uint32_t i = threadIdx.x; i < 5 * sc.n_rects; i += blockDim.x) lds_recs[i] = sc.recs[i];
         __syncthreads();
         MM_TS_STAGED();
         if constexpr (kLds == 3) {
             WpStack<kWW> st;
+            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
+        } else if constexpr (kLds == 9) {  // = 3 with u16 stack entries in scratch
+            ScratchStack16 st;
             chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
         } else if constexpr (kLds == 5) {
             WpStack<kWW> st;
@@ -395,7 +399,7 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
                                  : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
                                        (kLds == 5 ? 6 * (size_t)block * sizeof(float) : 0) +
                                        (kLds == 2 || kLds == 8 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
-                                       (kLds == 3 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
+                                       (kLds == 3 || kLds == 9 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves, kWW>
                             : k_trace_wavepersist<false, kLds, kBlock, kMinWaves, kWW>;
     int per_cu = 0, dev = 0, cus = 0;
@@ -430,7 +434,8 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
         MM_WP3(B, W, 32) }
     MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
     if (block == 1024 && min_waves == 8 && loop_form == 5) {
-        MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP2(8, 1024, 8, 5) MM_WP3(1024, 8, 5)
+        MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP2(8, 1024, 8, 5) MM_WP2(9, 1024, 8, 5)
+        MM_WP3(1024, 8, 5)
     }
     if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
     // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS

@@ -6,7 +6,7 @@ include/mm_api.h (HIP path) and include/mm_scene.h (C++ scene builder).
 from ._lib import (MM_EXT_ACCUMULATE, MM_EXT_COUNT_STATS, MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL,  # noqa: F401
                    MM_PIPE_WAVEFRONT, MMError, lib, mm_ext, mm_stats, mm_uniform)
 from .renderer import Renderer, make_ext  # noqa: F401
-from .scene import ChunkScheduler, Scene, calculate_quaternion, default_uniform  # noqa: F401
+from .scene import ChunkScheduler, Player, Scene, calculate_quaternion, check_collision, default_uniform  # noqa: F401
 
-__all__ = ["Renderer", "Scene", "ChunkScheduler", "default_uniform", "calculate_quaternion", "make_ext",
+__all__ = ["Renderer", "Scene", "ChunkScheduler", "Player", "check_collision", "default_uniform", "calculate_quaternion", "make_ext",
            "mm_ext", "mm_stats", "mm_uniform", "MMError", "lib"]

@@ -36,6 +36,7 @@ MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_THRESHOLD, MM_OPT_MIN_WAVES, MM_OPT_LDS_STACK = 1, 2, 3, 4, 5, 6
 MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS, MM_OPT_LDS_SPLIT, MM_OPT_COLD_LDS, MM_OPT_GLOBAL_RECTS = 7, 8, 9, 10, 11
 MM_OPT_FUSE_RESOLVE, MM_OPT_TAIL_GATE, MM_OPT_FAIR, MM_OPT_GRAB, MM_OPT_BLOCKSYNC = 12, 13, 14, 15, 16
+MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
 
@@ -70,6 +71,10 @@ class mm_stats(C.Structure):
 
 class mm_rng(C.Structure):
     _fields_ = [("key", C.c_uint32 * 8), ("counter", C.c_uint64), ("buf", C.c_uint32 * 64), ("pos", C.c_uint32)]
+
+
+class mm_player(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("quat", C.c_float * 4), ("half_theta", C.c_float), ("fps", C.c_float)]
 
 
 class mm_scene(C.Structure):
@@ -124,6 +129,12 @@ EXPORTS = {
     "mm_chunks_total": (C.c_uint32, [P]),
     "mm_chunks_next": (C.c_int, [P, C.c_uint32, P]),
     "mm_chunks_free": (None, [P]),
+    "mm_quat_mult": (None, [P, P, P]),
+    "mm_update_quat_angle": (None, [P, C.c_float, P]),
+    "mm_check_collision": (C.c_int, [P, C.c_uint32, P, P]),
+    "mm_player_init": (C.c_int, [P, C.POINTER(mm_player)]),
+    "mm_player_step": (C.c_int, [C.POINTER(mm_player), P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P]),
+    "mm_player_uniform": (C.c_int, [C.POINTER(mm_player), C.c_float, C.c_float, C.c_uint32, C.POINTER(mm_uniform)]),
     # mm_io.h
     "mm_write_ppm": (C.c_int, [C.c_char_p, P, C.c_uint32, C.c_uint32]),
     "mm_write_png": (C.c_int, [C.c_char_p, P, C.c_uint32, C.c_uint32]),

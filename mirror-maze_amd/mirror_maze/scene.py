@@ -114,3 +114,64 @@ class ChunkScheduler:
             self.close()
         except Exception:
             pass
+
+
+class Player:
+    """The reference's interactive camera (src/main.rs:738-842, 922-924):
+    WASD moves of 5/fps along the rotated axes, undone when the player box
+    (+-0.5, 0.2, 0.5) overlaps a BVH leaf (check_collision, main.rs:265-291),
+    mouse deltaX turning the view's half angle.  Drives an offline fly-through
+    (``uniform``) exactly as the reference's event loop drives its camera."""
+
+    KEY_A, KEY_S, KEY_D, KEY_W = 0, 1, 2, 13   # macOS key codes the reference matches
+
+    def __init__(self, scene: "Scene", view_w: float = 1024, view_h: float = 768):
+        self.scene = scene
+        self.view_w, self.view_h = view_w, view_h
+        u = default_uniform(view_w, view_h, 0)
+        self._p = _lib.mm_player()
+        q = np.array(list(u.cam.quat), dtype=np.float32)
+        check(lib().mm_player_init(q.ctypes.data, C.byref(self._p)))
+        self._nodes = np.ascontiguousarray(scene.nodes)
+
+    @property
+    def center(self) -> np.ndarray:
+        return np.array(list(self._p.center), dtype=np.float32)
+
+    @property
+    def quat(self) -> np.ndarray:
+        return np.array(list(self._p.quat), dtype=np.float32)
+
+    def step(self, keys=(), mouse_dx=()):
+        """One frame; returns the MM_PLAYER_* flags."""
+        k = np.ascontiguousarray(keys, dtype=np.uint16)
+        m = np.ascontiguousarray(mouse_dx, dtype=np.float32)
+        flags = C.c_uint32()
+        check(lib().mm_player_step(C.byref(self._p), k.ctypes.data if k.size else None, k.size,
+                                   m.ctypes.data if m.size else None, m.size, self._nodes.ctypes.data,
+                                   self._nodes.shape[0], C.byref(flags)))
+        return flags.value
+
+    def uniform(self, time: int = 0) -> _lib.mm_uniform:
+        u = _lib.mm_uniform()
+        check(lib().mm_player_uniform(C.byref(self._p), self.view_w, self.view_h, time, C.byref(u)))
+        return u
+
+
+def check_collision(nodes: np.ndarray, bmin, bmax) -> int:
+    """check_collision (src/main.rs:265-291): first leaf overlapping the box, or -1."""
+    nodes = np.ascontiguousarray(nodes)
+    a = np.asarray(bmin, dtype=np.float32)
+    b = np.asarray(bmax, dtype=np.float32)
+    r = lib().mm_check_collision(nodes.ctypes.data, nodes.shape[0], a.ctypes.data, b.ctypes.data)
+    if r == -2:
+        raise ValueError("check_collision: node index out of range")
+    return int(r)
+
+
+def quat_mult(v, q) -> np.ndarray:
+    a = np.asarray(v, dtype=np.float32)
+    b = np.asarray(q, dtype=np.float32)
+    out = np.zeros(3, dtype=np.float32)
+    lib().mm_quat_mult(a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out

@@ -303,3 +303,88 @@ def calculate_quaternion(d):
     ht = f32(math.asin(float(am))) / f32(2.0)
     s, c = f32(math.sin(float(ht))), f32(math.cos(float(ht)))
     return np.array([nx * s, ny * s, nz * s, c], dtype=np.float32)
+
+
+# ---- interactive camera and collision (src/maths.rs:159-178, src/main.rs:265-291,
+# 738-842, 922-924) ----------------------------------------------------------------
+def _quat_dot(a, b):
+    """quat_dot, src/maths.rs:169-173 (f32, left-to-right)."""
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    d = ax * bx + ay * by + az * bz
+    s = aw * bw - d
+    cx, cy, cz = ay * bz - az * by, az * bx - ax * bz, ax * by - ay * bx
+    vx = cx + (bx * aw + ax * bw)
+    vy = cy + (by * aw + ay * bw)
+    vz = cz + (bz * aw + az * bw)
+    return (vx, vy, vz, s)
+
+
+def quat_mult(v, q):
+    """quat_mult, src/maths.rs:175-178: q^-1 (v, 0) q."""
+    q = tuple(f32(x) for x in q)
+    inv = (-q[0], -q[1], -q[2], q[3])
+    r = _quat_dot(_quat_dot(inv, (f32(v[0]), f32(v[1]), f32(v[2]), f32(0.0))), q)
+    return np.array(r[:3], dtype=np.float32)
+
+
+def update_quat_angle(q, theta):
+    """update_quat_angle, src/maths.rs:159-162 (sin/acos in double, rounded)."""
+    theta = f32(theta)
+    ratio = f32(math.sin(float(theta))) / f32(math.sin(float(f32(math.acos(float(f32(q[3])))))))
+    return np.array([f32(q[0]) * ratio, f32(q[1]) * ratio, f32(q[2]) * ratio, f32(math.cos(float(theta)))],
+                    dtype=np.float32)
+
+
+def check_collision(nodes, bmin, bmax, i=0):
+    """check_collision, src/main.rs:265-291 over an (n, ) structured/tuple node
+    list [(mn, mx, left_first, count)]; returns the node index or None."""
+    mn, mx, lf, cnt = nodes[i]
+
+    def hit():
+        return all(bmin[a] <= mx[a] and bmax[a] >= mn[a] for a in range(3))
+
+    if cnt == 1:
+        return i if hit() else None
+    if not hit():
+        return None
+    r = check_collision(nodes, bmin, bmax, lf)
+    if r is not None:
+        return r
+    return check_collision(nodes, bmin, bmax, lf + 1)
+
+
+def player_step(center, quat, half_theta, keys, mouse_dx, nodes, fps=60.0):
+    """One frame of the reference's event loop for the camera (main.rs:786-838,
+    mouse 922-924).  Returns (center, quat, half_theta, collided, rotated)."""
+    c = np.array(center, dtype=np.float32)
+    prev = c.copy()
+    step = f32(5.0) / f32(fps)
+    for k in keys:
+        if k == 0:
+            c = c - quat_mult((step, 0, 0), quat)
+        elif k == 1:
+            c = c - quat_mult((0, 0, step), quat)
+        elif k == 2:
+            c = c + quat_mult((step, 0, 0), quat)
+        elif k == 13:
+            c = c + quat_mult((0, 0, step), quat)
+    diag = np.array([0.5, 0.2, 0.5], dtype=np.float32)
+    collided = check_collision(nodes, c - diag, c + diag) is not None
+    if collided:
+        c = prev
+    q = np.array(quat, dtype=np.float32)
+    rotated = False
+    h = f32(half_theta)
+    if len(mouse_dx):
+        pi = f32(math.pi)
+        for dx in mouse_dx:
+            x = h - f32(dx) / f32(512.0)
+            r = f32(math.fmod(float(x), float(pi)))
+            if r < 0:
+                r = r + pi
+            h = r
+        nq = update_quat_angle(q, h)
+        if not np.isnan(nq).any():
+            q, rotated = nq, True
+    return c, q, h, collided, rotated
