@@ -103,9 +103,20 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
         t.join()
     dt = time.perf_counter() - t0
     rays = sum(totals)
+    # the same loop on one core (SURVEY 8d asks for both), ~budget/4 seconds of rows
+    n1 = int(max(1, min(H, budget_s / 4 / row_s)))
+    t0 = time.perf_counter()
+    rays1 = 0
+    for y in range(0, H, max(1, H // n1))[:n1]:
+        _, s1 = o.trace_tile(u, ext, 0, y, W, 1)
+        rays1 += s1.rays
+    dt1 = time.perf_counter() - t0
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{len(sample_rows)} of {H} rows (every {stride}th) x {W} px x {ext.spp} spp, "
-                      f"{rays} rays in {dt:.1f} s; scalar C oracle -O2 -ffp-contract=off"}
+                      f"{rays} rays in {dt:.1f} s; scalar C oracle -O2 -ffp-contract=off",
+            "single_core": {"value": round(rays1 / dt1 / 1e6, 3), "unit": "Mrays/s",
+                            "sample": f"{n1} rows, {rays1} rays in {dt1:.1f} s"},
+            "host_cpus": os.cpu_count()}
 
 
 def main():
