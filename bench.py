@@ -181,6 +181,14 @@ def main():
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in rens]
     last = [0]
     active = [len(rens)]  # contexts the frames alternate over
+    progress_t = [time.perf_counter()]
+
+    def progress(msg):
+        # long runs (C5) print a line to stderr every ~20 s so a watchdog sees progress
+        now = time.perf_counter()
+        if now - progress_t[0] > 20.0:
+            progress_t[0] = now
+            print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
 
     acc_tile = (torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev)
                 if args.accumulate else None)
@@ -253,6 +261,8 @@ def main():
             acc_tile.zero_()
     for i in range(args.steps):
         step(i, i)
+        if args.steps > 20 and i % 8 == 7:
+            progress(f"timed frame {i + 1}/{args.steps} queued")
     if acc_tile is not None:
         gather_accumulated()  # C5: one gather of the accumulated frame, inside the timed region
     if gatherer:
@@ -274,6 +284,7 @@ def main():
     for i in range(args.steps):
         st = step(i, i, stats=True)
         rays += st.rays; paths += st.paths; visits += st.node_visits; rtests += st.rect_tests
+        progress(f"counting rays: frame {i + 1}/{args.steps}")
     drain()
     counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
     t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
