@@ -21,7 +21,8 @@
 using namespace mm;
 
 namespace mm {
-size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out);
+size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
+                           size_t* n_slow);
 }
 
 struct mm_ctx {
@@ -41,6 +42,7 @@ struct mm_ctx {
     float4* d_shade = nullptr;
     uint2* d_recs = nullptr;    // compact leaf-ordered rect records
     size_t n_fast_recs = 0;
+    bool lean_ok = false;       // no SLOW rect records and every leaf holds one plane (loop form 7)
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
     bool has_scene = false;
@@ -337,9 +339,8 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_lds_stack = value;
             return MM_OK;
         case MM_OPT_TRAVERSAL:
-            if (value != -1 && value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 5 &&
-                value != 6 && value != 8 && value != 16 && value != 32)
-                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0-6, 8, 16 or 32");
+            if (value < -1 || (value > 7 && value != 8 && value != 16 && value != 32))
+                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0-7, 8, 16 or 32");
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
@@ -443,7 +444,8 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     HIPC(c, hipMalloc((void**)&c->d_shade, 2 * (size_t)n_rects * sizeof(float4)));
     HIPC(c, hipMalloc((void**)&c->d_idx, n_rects * sizeof(uint32_t)));
     std::vector<uint32_t> recs;
-    c->n_fast_recs = n_rects < (1u << 20) ? build_compact_rects(rects, n_rects, idx, recs) : 0;
+    size_t n_slow = n_rects;
+    c->n_fast_recs = n_rects < (1u << 20) ? build_compact_rects(rects, n_rects, idx, recs, &n_slow) : 0;
     if (n_rects >= (1u << 20)) recs.assign(10 * (size_t)n_rects, 2u << 30);  // all SLOW (index does not fit)
     HIPC(c, hipMalloc((void**)&c->d_recs, recs.size() * sizeof(uint32_t)));
     HIPC(c, hipMemcpyAsync(c->d_recs, recs.data(), recs.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
@@ -461,6 +463,12 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     c->depth = depth;
     c->stack16_ok = stack16 && (c->root_packed >> 24) < 16u && (c->root_packed & 0xFFFFFFu) < 4096u;
     c->fast_ok = fast;
+    {
+        bool single = true;
+        for (uint32_t i = 0; i < n_nodes; ++i)
+            if (nodes[i].count > 1) single = false;
+        c->lean_ok = single && n_slow == 0;
+    }
     c->has_scene = true;
     return MM_OK;
 }
@@ -646,8 +654,8 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                                                    "(256/8, 512/6, 512/8, 1024/1, 1024/8)");
             // loop form: auto = leaf+interior per iteration (measured 10.35 vs 11.06 ms on C3,
             // profiles/r01_ab_leafinterior.txt) where it is instantiated, else if-if
-            const int ww = c->opt_ww >= 0 ? c->opt_ww
-                                          : ((block == 1024 && c->opt_min_waves == 8 && !c->opt_cold_lds) ? 5 : 0);
+            int ww = c->opt_ww >= 0 ? c->opt_ww
+                                    : ((block == 1024 && c->opt_min_waves == 8 && !c->opt_cold_lds) ? 5 : 0);
             const uint32_t slots = std::max(1u, c->depth);
             // LDS per block that keeps the launch-bound occupancy (min_waves per SIMD, 4 SIMDs):
             // 1024/8 and 768/6 -> 2 blocks per CU -> 80 KB each
@@ -661,7 +669,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
             if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= lds_budget)
                 mode = 5;
-            if (mode == 1 && (ww == 0 || ww == 5) && c->opt_glob_rects == 1) mode = 7;
+            if (mode == 1 && (ww == 0 || ww == 5 || ww == 7) && c->opt_glob_rects == 1) mode = 7;
             // LDS stack beside the nodes, compact rect records through L1/L2 (loop form 5)
             if (lds_fits && ww == 5 && c->opt_lds_stack == 2 && c->stack16_ok && block == 1024 &&
                 c->opt_min_waves == 8 && lds_total <= lds_budget)
@@ -671,15 +679,19 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                 c->opt_min_waves == 8)
                 mode = 9;
             DevScene sc = dev_scene(c);
-            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6) &&
+            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6 || ww == 7) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
                 // nodes exceed the LDS budget (or an explicit cache size is set):
                 // cache the top of the breadth-first array
                 const size_t budget = c->opt_lds_split == 1 ? lds_budget
                                                             : (size_t)c->opt_lds_split * 1024;
                 sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
-                mode = ((ww == 0 || ww == 5) && c->opt_glob_rects != 0) ? 6 : 4;
+                mode = ((ww == 0 || ww == 5 || ww == 7) && c->opt_glob_rects != 0) ? 6 : 4;
             }
+            // the lean form needs compact records for every leaf (modes 3, 6, 7) and a lean scene
+            if (ww == 7 && (!c->lean_ok || block != 1024 || c->opt_min_waves != 8 ||
+                            (mode != 3 && mode != 6 && mode != 7)))
+                ww = 5;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, slots,

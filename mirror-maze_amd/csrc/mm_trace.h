@@ -250,6 +250,26 @@ __device__ __forceinline__ void rect_test_compact(const DevScene& sc, const R& r
     }
 }
 
+// Branch-free leaf test for scenes whose records are all FAST or SKIP (SKIP
+// records carry thresholds no x1 passes, rect_compact.cpp): the same
+// operations as rect_test_compact's FAST case.
+template <typename R>
+__device__ __forceinline__ void rect_test_compact_lean(const R& recs, uint32_t slot, const Ray& r, float& t,
+                                                       uint32_t& index) {
+    const uint2 w01 = recs[5 * slot + 0], w23 = recs[5 * slot + 1], w45 = recs[5 * slot + 2],
+                w67 = recs[5 * slot + 3], w89 = recs[5 * slot + 4];
+    const uint32_t meta = w89.y;
+    const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
+    const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
+    const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
+    const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
+    if (x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) && x2 >= __uint_as_float(w67.y) &&
+        x2 <= __uint_as_float(w89.x) && a > 0.1f && a < t) {
+        t = a;
+        index = meta & 0xFFFFFu;
+    }
+}
+
 template <bool kFast, typename V>
 __device__ __forceinline__ void leaf_tests(const DevScene& sc, const V& v, uint32_t lf, uint32_t cnt, const Ray& r,
                                            float& t, uint32_t& index) {
@@ -393,6 +413,45 @@ __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, cons
                     if (head >= stack_cap(stack)) return false;
                     stack.push(head++, sw ? pl : pr);
                 }
+            }
+        }
+    }
+    return true;
+}
+
+// Lean leaf-then-interior form (MM_OPT_TRAVERSAL 7) for scenes where every
+// leaf holds one plane and no rect record is SLOW (mm_upload_scene sets
+// lean_ok): the leaf test is rect_test_compact_lean (no kind branches, no
+// per-leaf loop) and pushes skip the overflow test (upload rejects trees
+// deeper than the stack; near-first traversal holds at most one pending far
+// child per level).  Per lane the operation sequence is traverse_li's.
+template <bool kStats, typename V, typename Stack>
+__device__ __forceinline__ bool traverse_lil(const DevScene& sc, const V& v, const Ray& r, float& t,
+                                             uint32_t& index, Stack& stack, Counters& c) {
+    uint32_t cur = sc.root_packed, head = 0;
+    for (;;) {
+        if ((cur >> 24) != 0) {
+            rect_test_compact_lean(v.recs, cur & 0xFFFFFFu, r, t, index);
+            if (kStats) c.rtests++;
+            if (head == 0) break;
+            cur = stack.pop(--head);
+        }
+        if ((cur >> 24) == 0) {
+            const uint32_t lf = cur & 0xFFFFFFu;
+            if (kStats) c.visits++;
+            float4 la, lb, ra, rb;
+            node_pair(v.nodes, lf, la, lb, ra, rb);
+            const float d1 = aabb_pairs<true>(la, lb, r, t);
+            const float d2 = aabb_pairs<true>(ra, rb, r, t);
+            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+            const bool sw = d1 > d2;
+            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
+            if (dn == kBig) {
+                if (head == 0) break;
+                cur = stack.pop(--head);
+            } else {
+                cur = sw ? pr : pl;
+                if (df != kBig) stack.push(head++, sw ? pl : pr);
             }
         }
     }
@@ -549,6 +608,9 @@ __device__ __forceinline__ bool closest_hit(const DevScene& sc, const V& v, F3 o
     } else if constexpr (kWW >= 8) {
         if (sc.fast_ok && ray_fast_ok(r)) return traverse_lb<true, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
         return traverse_lb<false, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
+    } else if constexpr (kWW == 7) {
+        if (sc.fast_ok && ray_fast_ok(r)) return traverse_lil<kStats>(sc, v, r, t, index, stack, c);
+        return traverse_li<false, kStats>(sc, v, r, t, index, stack, c);
     } else if constexpr (kWW == 5) {
         if (sc.fast_ok && ray_fast_ok(r)) return traverse_li<true, kStats>(sc, v, r, t, index, stack, c);
         return traverse_li<false, kStats>(sc, v, r, t, index, stack, c);

@@ -82,9 +82,10 @@ int single_axis(V3 v) {
 // kind: 0 FAST, 1 SKIP (zero-length: never hits), 2 SLOW (general test).
 constexpr uint32_t kRecWords = 10;
 
-size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out) {
+size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
+                           size_t* n_slow) {
     std::vector<uint32_t> per(kRecWords * (size_t)n_rects, 0);
-    size_t n_fast = 0;
+    size_t n_fast = 0, slow = 0;
     for (uint32_t k = 0; k < n_rects; ++k) {
         const mm_rect& r = rects[k];
         const V3 o{r.o[0], r.o[1], r.o[2]}, v{r.v[0], r.v[1], r.v[2]}, u{r.u[0], r.u[1], r.u[2]};
@@ -97,6 +98,12 @@ size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_
         const float lv = std::sqrt(dot3(v, v)), lu = std::sqrt(dot3(u, u));
         if (std::isnan(n.x) || std::isnan(n.y) || std::isnan(n.z)) {
             kind = 1;  // zero-length wall: nc is NaN, `nc != 0` true but a = NaN fails a > 0.1
+            // Also a valid FAST record that can never hit (thresholds lo = +inf,
+            // hi = -inf fail for every x1, NaN included), for the branch-free
+            // leaf test of scenes without SLOW records (rect_test_compact_lean).
+            const float never[9] = {0.0f, 0.0f, 0.0f, 1.0f, 1.0f, INFINITY, -INFINITY, INFINITY, -INFINITY};
+            for (int j = 0; j < 9; ++j) w[j] = f2u(never[j]);
+            ak = 0; av = 1; au = 2;
         } else {
             const int iv = single_axis(v), iu = single_axis(u);
             if (iv >= 0 && iu >= 0 && iv != iu) {
@@ -116,11 +123,13 @@ size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_
             }
         }
         if (kind == 0) ++n_fast;
+        if (kind == 2) ++slow;
         w[9] = (k & 0xFFFFFu) | (ak << 20) | (av << 22) | (au << 24) | (kind << 30);
     }
     out.assign(kRecWords * (size_t)n_rects, 0);
     for (uint32_t s = 0; s < n_rects; ++s)
         std::memcpy(&out[kRecWords * (size_t)s], &per[kRecWords * (size_t)idx[s]], kRecWords * 4);
+    if (n_slow) *n_slow = slow;
     return n_fast;
 }
 

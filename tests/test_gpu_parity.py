@@ -138,6 +138,8 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "ifif-ldsrects": (1, {1: 1, 3: 2, 7: 0, 8: 1}),
     "leafinterior-grab3-fair": (1, {1: 1, 3: 2, 7: 5, 15: 3, 14: 1}),
     "blocksync": (1, {3: 2, 16: 1}),
+    "leanli": (1, {3: 2, 7: 7}),
+    "leanli-split2kb": (1, {3: 2, 7: 7, 9: 2}),
     "blocksync-nofuse": (1, {3: 2, 16: 1, 12: 0}),
     "leafinterior-lds": (1, {1: 1, 3: 2, 7: 5, 8: 0, 11: 0}),
     "leafinterior-split2kb": (1, {1: 1, 3: 2, 7: 5, 9: 2}),
@@ -182,7 +184,7 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
 @pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
                                   "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
                                   "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
-                                  "leafinterior-grab3-fair", "blocksync"])
+                                  "leafinterior-grab3-fair", "blocksync", "leanli"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -297,9 +299,9 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}],
+@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}, {7: 7}],
                          ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects",
-                              "leafinterior", "ifif"])
+                              "leafinterior", "ifif", "leanli"])
 def test_large_scene_top_of_tree_cache(gpu, opts):
     """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
     default kernel caches the top of the breadth-first node array in LDS and
