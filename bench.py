@@ -34,6 +34,7 @@ sys.path.insert(0, str(REPO))
 
 CONFIGS = {
     # id: (maze_n, W, H, spp, bounce_limit, mirror_limit, description)
+    "c1": (16, 256, 256, 1, 1, 15, "C1: 16x16 maze, 256x256, 1 spp, 1 bounce"),
     "c2": (16, 1920, 1080, 1, 4, 15, "C2: 16x16 maze, 1920x1080, 1 spp, 4 bounces"),
     "c3": (32, 1920, 1080, 8, 8, 8, "C3: 32x32 maze, 1920x1080, 8 spp, 8 mirror bounces"),
     "c4": (32, 3840, 2160, 16, 8, 15, "C4: 32x32 maze, 3840x2160, 16 spp, 8 bounces"),
