@@ -135,7 +135,14 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   3 if-if with the stack top in a register,
                                   4 if-if, lanes refilled with new paths at every bounce,
                                   5 leaf tests and the next interior step in one iteration (1024/8 only),
-                                  -1 auto: 5 at 1024 threads / 8 waves, else 0 (default)
+                                  6 bounce refill with form 5's traversal,
+                                  7 form 5 with branch-free compact leaf tests and no push overflow test
+                                    (scenes without SLOW rect records),
+                                  9 verified conservative search (approximate slab quotients on expanded
+                                    boxes, exact rect tests, exact check of the winner's leaf box;
+                                    bit-identical results, slower on the maze: experimental),
+                                  -1 auto: 7 when the scene allows, else 5 at 1024 threads / 8 waves,
+                                    else 0 (default)
                                   8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
 #define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
 #define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 2 the same

@@ -42,6 +42,11 @@ struct DevScene {
     uint32_t root_packed;     // count<<24 | left_first of node 0
     uint32_t fast_ok;         // scene coordinates inside the Markstein guard
     const uint2* recs;        // 5 x uint2 per BVH slot: compact rect records (rect_compact.cpp)
+    // Verified conservative search (MM_OPT_TRAVERSAL 9): `nodes` then holds the
+    // boxes expanded by cons_margin, these the exact ones and each slot's leaf box
+    const float4* nodes_exact;  // 2 * n_nodes, production layout, exact bounds
+    const float4* slot_box;     // 2 per slot: (mn.x, mx.x, mn.y, mx.y), (mn.z, mx.z, 0, 0) of its leaf
+    float cons_bound;           // |ray origin component| must be <= this for the search (else exact)
 };
 
 // ---- IEEE helpers (the AIR intrinsics with their IEEE meaning) -------------

@@ -42,7 +42,10 @@ struct mm_ctx {
     float4* d_shade = nullptr;
     uint2* d_recs = nullptr;    // compact leaf-ordered rect records
     size_t n_fast_recs = 0;
-    bool lean_ok = false;       // no SLOW rect records and every leaf holds one plane (loop form 7)
+    bool lean_ok = false;       // no SLOW rect records (loop forms 7, 9)
+    float4* d_nodes_cons = nullptr;  // production layout, boxes expanded by the search margin (form 9)
+    float4* d_slot_box = nullptr;    // per BVH slot: its leaf's exact box (form 9 verification)
+    float cons_bound = 0.0f;         // |coordinate| bound of the scene (form 9 ray guard)
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
     bool has_scene = false;
@@ -129,6 +132,9 @@ DevScene dev_scene(const mm_ctx* c) {
     s.fast_ok = c->fast_ok ? 1u : 0u;
     s.geo = c->d_geo;
     s.recs = c->d_recs;
+    s.nodes_exact = c->d_nodes;
+    s.slot_box = c->d_slot_box;
+    s.cons_bound = c->cons_bound;
     s.shade = c->d_shade;
     s.idx = c->d_idx;
     s.n_nodes = c->n_nodes;
@@ -139,6 +145,8 @@ DevScene dev_scene(const mm_ctx* c) {
 void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_nodes_ref); (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
+    (void)hipFree(c->d_nodes_cons); (void)hipFree(c->d_slot_box);
+    c->d_nodes_cons = nullptr; c->d_slot_box = nullptr;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
     c->has_scene = false;
 }
@@ -339,8 +347,8 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_lds_stack = value;
             return MM_OK;
         case MM_OPT_TRAVERSAL:
-            if (value < -1 || (value > 7 && value != 8 && value != 16 && value != 32))
-                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0-7, 8, 16 or 32");
+            if (value < -1 || (value > 9 && value != 16 && value != 32))
+                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0-9, 16 or 32");
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
@@ -424,6 +432,30 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
             packed[2 * i] = make_float4(nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1]);
             packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
         }
+    // Verified conservative search (form 9): boxes expanded outward by
+    // E = C * 2^-14, C = the scene's largest |coordinate| (>= 64x the rounding
+    // bound of mm_trace.h: traverse_cons), and each slot's exact leaf box.
+    float cbound = 1.0f;
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        for (int a = 0; a < 3; ++a) cbound = std::max(cbound, std::max(std::fabs(nodes[i].mn[a]), std::fabs(nodes[i].mx[a])));
+    const double margin = (double)cbound * 0x1p-14;
+    auto dn = [&](float x) { return std::nextafter((float)((double)x - margin), -INFINITY); };
+    auto up = [&](float x) { return std::nextafter((float)((double)x + margin), INFINITY); };
+    std::vector<float4> packed_cons(packed);
+    for (size_t i = 4; i < packed_cons.size(); i += 2) {
+        float4& a = packed_cons[i];
+        float4& b = packed_cons[i + 1];
+        a = make_float4(dn(a.x), up(a.y), dn(a.z), up(a.w));
+        b = make_float4(dn(b.x), up(b.y), b.z, b.w);
+    }
+    std::vector<float4> slot_box(2 * (size_t)n_rects, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        if (nodes[i].count > 0)
+            for (uint32_t j = 0; j < nodes[i].count; ++j) {
+                const uint32_t sl = nodes[i].left_first + j;
+                slot_box[2 * (size_t)sl] = make_float4(nodes[i].mn[0], nodes[i].mx[0], nodes[i].mn[1], nodes[i].mx[1]);
+                slot_box[2 * (size_t)sl + 1] = make_float4(nodes[i].mn[2], nodes[i].mx[2], 0.0f, 0.0f);
+            }
     bool fast = true;
     for (uint32_t i = 0; i < n_nodes && fast; ++i)
         for (int a = 0; a < 3; ++a) fast = fast && coord_ok(nodes[i].mn[a]) && coord_ok(nodes[i].mx[a]);
@@ -453,6 +485,12 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     // mm_node is exactly two float4: (mn.xyz, mx.x) (mx.yz, left_first, count)
     HIPC(c, hipMemcpyAsync(c->d_nodes_ref, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_nodes, packed.data(), packed.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMalloc((void**)&c->d_nodes_cons, packed_cons.size() * sizeof(float4)));
+    HIPC(c, hipMemcpyAsync(c->d_nodes_cons, packed_cons.data(), packed_cons.size() * sizeof(float4),
+                           hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMalloc((void**)&c->d_slot_box, slot_box.size() * sizeof(float4)));
+    HIPC(c, hipMemcpyAsync(c->d_slot_box, slot_box.data(), slot_box.size() * sizeof(float4), hipMemcpyHostToDevice,
+                           c->stream));
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_idx, idx, n_rects * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
@@ -463,12 +501,8 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     c->depth = depth;
     c->stack16_ok = stack16 && (c->root_packed >> 24) < 16u && (c->root_packed & 0xFFFFFFu) < 4096u;
     c->fast_ok = fast;
-    {
-        bool single = true;
-        for (uint32_t i = 0; i < n_nodes; ++i)
-            if (nodes[i].count > 1) single = false;
-        c->lean_ok = single && n_slow == 0;
-    }
+    c->cons_bound = cbound;
+    c->lean_ok = n_slow == 0;
     c->has_scene = true;
     return MM_OK;
 }
@@ -653,7 +687,8 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                 return fail(c, MM_ERR_UNSUPPORTED, "wave-persistent kernel: block/min-waves pair not instantiated "
                                                    "(256/8, 512/6, 512/8, 1024/1, 1024/8)");
             // loop form: auto = leaf+interior per iteration (measured 10.35 vs 11.06 ms on C3,
-            // profiles/r01_ab_leafinterior.txt) where it is instantiated, else if-if
+            // profiles/r01_ab_leafinterior.txt) where it is instantiated, its lean form (7)
+            // when the scene allows (below), else if-if
             int ww = c->opt_ww >= 0 ? c->opt_ww
                                     : ((block == 1024 && c->opt_min_waves == 8 && !c->opt_cold_lds) ? 5 : 0);
             const uint32_t slots = std::max(1u, c->depth);
@@ -669,7 +704,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
             if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= lds_budget)
                 mode = 5;
-            if (mode == 1 && (ww == 0 || ww == 5 || ww == 7) && c->opt_glob_rects == 1) mode = 7;
+            if (mode == 1 && (ww == 0 || ww == 5 || ww == 7 || ww == 9) && c->opt_glob_rects == 1) mode = 7;
             // LDS stack beside the nodes, compact rect records through L1/L2 (loop form 5)
             if (lds_fits && ww == 5 && c->opt_lds_stack == 2 && c->stack16_ok && block == 1024 &&
                 c->opt_min_waves == 8 && lds_total <= lds_budget)
@@ -679,19 +714,24 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                 c->opt_min_waves == 8)
                 mode = 9;
             DevScene sc = dev_scene(c);
-            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6 || ww == 7) &&
+            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6 || ww == 7 || ww == 9) &&
                 (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
                 // nodes exceed the LDS budget (or an explicit cache size is set):
                 // cache the top of the breadth-first array
                 const size_t budget = c->opt_lds_split == 1 ? lds_budget
                                                             : (size_t)c->opt_lds_split * 1024;
                 sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
-                mode = ((ww == 0 || ww == 5 || ww == 7) && c->opt_glob_rects != 0) ? 6 : 4;
+                mode = ((ww == 0 || ww == 5 || ww == 7 || ww == 9) && c->opt_glob_rects != 0) ? 6 : 4;
             }
-            // the lean form needs compact records for every leaf (modes 3, 6, 7) and a lean scene
-            if (ww == 7 && (!c->lean_ok || block != 1024 || c->opt_min_waves != 8 ||
-                            (mode != 3 && mode != 6 && mode != 7)))
-                ww = 5;
+            // the lean and verified-search forms need compact records for every leaf (modes 3,
+            // 6, 7) and a lean scene (no SLOW records); auto prefers the lean form
+            // (C3 10.40 -> 9.56 ms, profiles/r01_ab_lean.txt)
+            const bool lean_fits = c->lean_ok && block == 1024 && c->opt_min_waves == 8 &&
+                                   (mode == 3 || mode == 6 || mode == 7);
+            // (auto: not with the split node cache, where it measured 30.6 vs 29.4 ms on the C5 scene)
+            if (c->opt_ww < 0 && ww == 5 && lean_fits && mode != 6) ww = 7;
+            if ((ww == 7 || ww == 9) && !lean_fits) ww = 5;
+            if (ww == 9) sc.nodes = c->d_nodes_cons;  // the search's expanded boxes (LDS and global)
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, slots,

@@ -419,10 +419,9 @@ __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, cons
     return true;
 }
 
-// Lean leaf-then-interior form (MM_OPT_TRAVERSAL 7) for scenes where every
-// leaf holds one plane and no rect record is SLOW (mm_upload_scene sets
-// lean_ok): the leaf test is rect_test_compact_lean (no kind branches, no
-// per-leaf loop) and pushes skip the overflow test (upload rejects trees
+// Lean leaf-then-interior form (MM_OPT_TRAVERSAL 7) for scenes without SLOW
+// rect records (mm_upload_scene sets lean_ok): the leaf test is
+// rect_test_compact_lean (no kind branches) and pushes skip the overflow test (upload rejects trees
 // deeper than the stack; near-first traversal holds at most one pending far
 // child per level).  Per lane the operation sequence is traverse_li's.
 template <bool kStats, typename V, typename Stack>
@@ -431,8 +430,9 @@ __device__ __forceinline__ bool traverse_lil(const DevScene& sc, const V& v, con
     uint32_t cur = sc.root_packed, head = 0;
     for (;;) {
         if ((cur >> 24) != 0) {
-            rect_test_compact_lean(v.recs, cur & 0xFFFFFFu, r, t, index);
-            if (kStats) c.rtests++;
+            const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+            for (uint32_t i = 0; i < cnt; ++i) rect_test_compact_lean(v.recs, lf + i, r, t, index);
+            if (kStats) c.rtests += cnt;
             if (head == 0) break;
             cur = stack.pop(--head);
         }
@@ -456,6 +456,134 @@ __device__ __forceinline__ bool traverse_lil(const DevScene& sc, const V& v, con
         }
     }
     return true;
+}
+
+// ---------------------------------------------------------------------------
+// Verified conservative closest hit (MM_OPT_TRAVERSAL 9).
+//
+// Search: the same BVH with every box expanded by an absolute margin E
+// (mm_upload_scene) and slab quotients RN(RN(b - o) * RN(1/d)) -- two
+// operations instead of the exact quotient's four -- culling only boxes whose
+// approximate interval starts beyond the best hit so far (<=, so ties
+// survive).  Every rect reached gets the exact reference test (the compact
+// record's operations) without its `a < t` clause; the minimum a* and its slot
+// are kept with a tie flag.
+//
+// Why the search cannot miss the reference's answer: a rect the reference
+// accepts at a has o + a*d within delta <= ~10u*C of the rect per axis
+// (u = 2^-24, C >= every |coordinate| and |origin component|), so inside its
+// leaf box, and every ancestor box, expanded by E, with margin E - delta; an
+// approximate quotient is within 3u*|b - o|/|d| <= 6u*C/|d| of the exact one,
+// so with E >= 64*(10u + 6u)*C the approximate interval of every expanded
+// ancestor contains a.  Hence a* is the minimum over ALL rects the reference
+// would accept at any t, and a tie flag is exact.
+//
+// Verification (exactness of the answer, not of the search): with a* unique,
+// the reference's current best is > a* whenever it tests a box on R*'s path,
+// and the exact (reference-arithmetic) slab values of every ancestor box
+// bracket those of R*'s leaf box (RN and Markstein division are monotone,
+// ancestors contain the leaf).  So if the leaf box's exact test gives
+// tmax >= tmin, tmax > 0 and tmin <= a*, the reference reaches R*, accepts it,
+// and never replaces it: its answer is (a*, R*).  A tie, a failed check, or a
+// ray outside the guards runs traverse_li on the exact nodes instead.
+// scripts/cons_sim.cpp replays C3 / C5 / P0 frames on the CPU: 0 mismatches
+// in 37 M queries, ties only where coplanar rects overlap (P0's outer walls).
+
+// RN(RN(b - o) * y): the approximate slab quotient
+__device__ __forceinline__ float qapprox(float b, float o, float y) { return (b - o) * y; }
+
+__device__ __forceinline__ float aabb_cons(float4 a, float4 b, const Ray& r, float best) {
+    const float tx1 = qapprox(a.x, r.o.x, r.y.x), tx2 = qapprox(a.y, r.o.x, r.y.x);
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    const float ty1 = qapprox(a.z, r.o.y, r.y.y), ty2 = qapprox(a.w, r.o.y, r.y.y);
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    tmax = fminf(tmax, fmaxf(ty1, ty2));
+    const float tz1 = qapprox(b.x, r.o.z, r.y.z), tz2 = qapprox(b.y, r.o.z, r.y.z);
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    tmax = fminf(tmax, fmaxf(tz1, tz2));
+    return (tmax >= tmin && tmin <= best && tmax > 0.0f) ? tmin : kBig;
+}
+
+// Exact compact rect test (FAST / SKIP records) without the `a < t` clause:
+// a if the reference would accept the rect at a large enough t, else kBig.
+template <typename R>
+__device__ __forceinline__ float rect_a_compact(const R& recs, uint32_t slot, const Ray& r) {
+    const uint2 w01 = recs[5 * slot + 0], w23 = recs[5 * slot + 1], w45 = recs[5 * slot + 2],
+                w67 = recs[5 * slot + 3], w89 = recs[5 * slot + 4];
+    const uint32_t meta = w89.y;
+    const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
+    const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
+    const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
+    const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
+    const bool hit = x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) &&
+                     x2 >= __uint_as_float(w67.y) && x2 <= __uint_as_float(w89.x) && a > 0.1f;
+    return hit ? a : kBig;
+}
+
+__device__ __forceinline__ bool cons_ray_ok(const DevScene& sc, const Ray& r) {
+    return fabsf(r.o.x) <= sc.cons_bound && fabsf(r.o.y) <= sc.cons_bound && fabsf(r.o.z) <= sc.cons_bound;
+}
+
+template <bool kStats, typename V, typename Stack>
+__device__ __forceinline__ bool traverse_cons(const DevScene& sc, const V& v, const Ray& r, float& t,
+                                              uint32_t& index, Stack& stack, Counters& c) {
+    uint32_t cur = sc.root_packed, head = 0, bslot = 0;
+    float best = kBig;
+    bool tie = false;
+    for (;;) {
+        if ((cur >> 24) != 0) {
+            const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
+            for (uint32_t i = 0; i < cnt; ++i) {
+                const float a = rect_a_compact(v.recs, lf + i, r);
+                tie = tie || (a == best && a != kBig);
+                if (a < best) {
+                    best = a;
+                    bslot = lf + i;
+                    tie = false;
+                }
+            }
+            if (kStats) c.rtests += cnt;
+            if (head == 0) break;
+            cur = stack.pop(--head);
+        }
+        if ((cur >> 24) == 0) {
+            const uint32_t lf = cur & 0xFFFFFFu;
+            if (kStats) c.visits++;
+            float4 la, lb, ra, rb;
+            node_pair(v.nodes, lf, la, lb, ra, rb);
+            const float d1 = aabb_cons(la, lb, r, best);
+            const float d2 = aabb_cons(ra, rb, r, best);
+            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+            const bool sw = d1 > d2;
+            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
+            if (dn == kBig) {
+                if (head == 0) break;
+                cur = stack.pop(--head);
+            } else {
+                cur = sw ? pr : pl;
+                if (df != kBig) stack.push(head++, sw ? pl : pr);
+            }
+        }
+    }
+    if (best == kBig) return true;  // no rect hit: (kBig, index untouched)
+    if (!tie) {
+        const float4 a = sc.slot_box[2 * bslot], b = sc.slot_box[2 * bslot + 1];
+        const float tx1 = qdiv(a.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(a.y - r.o.x, r.d.x, r.y.x);
+        float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+        const float ty1 = qdiv(a.z - r.o.y, r.d.y, r.y.y), ty2 = qdiv(a.w - r.o.y, r.d.y, r.y.y);
+        tmin = fmaxf(tmin, fminf(ty1, ty2));
+        tmax = fminf(tmax, fmaxf(ty1, ty2));
+        const float tz1 = qdiv(b.x - r.o.z, r.d.z, r.y.z), tz2 = qdiv(b.y - r.o.z, r.d.z, r.y.z);
+        tmin = fmaxf(tmin, fminf(tz1, tz2));
+        tmax = fminf(tmax, fmaxf(tz1, tz2));
+        if (tmax >= tmin && tmax > 0.0f && tmin <= best) {
+            t = best;
+            index = v.recs[5 * bslot + 4].y & 0xFFFFFu;
+            return true;
+        }
+    }
+    // tie or unverified: the reference query on the exact nodes (global memory)
+    return traverse_li<true, false>(sc, view(sc.nodes_exact, v.recs), r, t, index, stack, c);
 }
 
 // "while-while" form of the same traversal: each lane runs interior steps
@@ -605,9 +733,13 @@ __device__ __forceinline__ bool closest_hit(const DevScene& sc, const V& v, F3 o
     if constexpr (kWW == 2) {
         if (sc.fast_ok && ray_fast_ok(r)) return traverse_lean<true, kStats>(sc, v, r, t, index, stack, c);
         return traverse_lean<false, kStats>(sc, v, r, t, index, stack, c);
-    } else if constexpr (kWW >= 8) {
+    } else if constexpr (kWW >= 8 && kWW != 9) {
         if (sc.fast_ok && ray_fast_ok(r)) return traverse_lb<true, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
         return traverse_lb<false, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
+    } else if constexpr (kWW == 9) {
+        if (sc.fast_ok && ray_fast_ok(r) && cons_ray_ok(sc, r))
+            return traverse_cons<kStats>(sc, v, r, t, index, stack, c);
+        return traverse_li<false, kStats>(sc, view(sc.nodes_exact, v.recs), r, t, index, stack, c);
     } else if constexpr (kWW == 7) {
         if (sc.fast_ok && ray_fast_ok(r)) return traverse_lil<kStats>(sc, v, r, t, index, stack, c);
         return traverse_li<false, kStats>(sc, v, r, t, index, stack, c);

@@ -439,6 +439,7 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
     }
     if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
     if (block == 1024 && min_waves == 8 && loop_form == 7) { MM_WP2(3, 1024, 8, 7) MM_WP2(6, 1024, 8, 7) MM_WP2(7, 1024, 8, 7) }
+    if (block == 1024 && min_waves == 8 && loop_form == 9) { MM_WP2(3, 1024, 8, 9) MM_WP2(6, 1024, 8, 9) MM_WP2(7, 1024, 8, 9) }
     // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS
     if (block == 768 && min_waves == 6 && loop_form == 5) { MM_WP2(3, 768, 6, 5) MM_WP2(6, 768, 6, 5) }
 #undef MM_WP

@@ -69,6 +69,7 @@ VARIANTS["li-b768-w6"] = dict(pipe=1, persist=2, lds=1, block=768, mw=6, ls=0, l
 VARIANTS["brli-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=6)
 VARIANTS["blocksync"] = dict(pipe=1, bsync=1)
 VARIANTS["lean7"] = dict(pipe=1, ww=7)
+VARIANTS["cons9"] = dict(pipe=1, ww=9)
 VARIANTS["li-ldsstack-grec"] = dict(pipe=1, ls=2)
 VARIANTS["li-ldsstack"] = dict(pipe=1, ls=1, lr=0)
 VARIANTS["li-lds-grec"] = dict(pipe=1, lr=0, gr=1)

@@ -139,6 +139,9 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "leafinterior-grab3-fair": (1, {1: 1, 3: 2, 7: 5, 15: 3, 14: 1}),
     "blocksync": (1, {3: 2, 16: 1}),
     "leanli": (1, {3: 2, 7: 7}),
+    "cons": (1, {3: 2, 7: 9}),
+    "cons-split2kb": (1, {3: 2, 7: 9, 9: 2}),
+    "cons-globalrects": (1, {3: 2, 7: 9, 8: 0, 11: 1}),
     "leanli-split2kb": (1, {3: 2, 7: 7, 9: 2}),
     "blocksync-nofuse": (1, {3: 2, 16: 1, 12: 0}),
     "leafinterior-lds": (1, {1: 1, 3: 2, 7: 5, 8: 0, 11: 0}),
@@ -176,15 +179,18 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
         got, st = ren.trace_tile(u, e, x0, y0, w, h, stats=True)
         ref, rst = o.trace_tile(u, e, x0, y0, w, h)
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
-        assert (st.rays, st.node_visits, st.rect_tests, st.paths) == \
-               (rst.rays, rst.node_visits, rst.rect_tests, rst.paths)
+        if pipe.startswith("cons"):  # the verified search does its own (larger) amount of work
+            assert (st.rays, st.paths) == (rst.rays, rst.paths)
+        else:
+            assert (st.rays, st.node_visits, st.rect_tests, st.paths) == \
+                   (rst.rays, rst.node_visits, rst.rect_tests, rst.paths)
     ren.close()
 
 
 @pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
                                   "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
                                   "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
-                                  "leafinterior-grab3-fair", "blocksync", "leanli"])
+                                  "leafinterior-grab3-fair", "blocksync", "leanli", "cons"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -299,9 +305,9 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}, {7: 7}],
+@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}, {7: 7}, {7: 9}],
                          ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects",
-                              "leafinterior", "ifif", "leanli"])
+                              "leafinterior", "ifif", "leanli", "cons"])
 def test_large_scene_top_of_tree_cache(gpu, opts):
     """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
     default kernel caches the top of the breadth-first node array in LDS and
@@ -322,7 +328,10 @@ def test_large_scene_top_of_tree_cache(gpu, opts):
         got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
         ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
-        assert (st.rays, st.node_visits, st.rect_tests) == (rst.rays, rst.node_visits, rst.rect_tests)
+        if opts.get(7) == 9:  # the verified search does its own (larger) amount of work
+            assert st.rays == rst.rays
+        else:
+            assert (st.rays, st.node_visits, st.rect_tests) == (rst.rays, rst.node_visits, rst.rect_tests)
     r.close()
 
 
