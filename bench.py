@@ -249,7 +249,7 @@ def main():
                 if distributed:
                     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
                 calib[m] = min(calib.get(m, 1e9), float(dt.item()) / 6 * 1e3)
-        active[0] = 2 if calib[2] < 0.98 * calib[1] else 1  # overlap only for a clear gain
+        active[0] = 2 if calib[2] < 0.99 * calib[1] else 1  # overlap only for a clear (>1 %) gain
     for r in rens[:active[0]]:
         r.set_profiling(True)
         r.kernel_timing(reset=True)

@@ -168,6 +168,11 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_BLOCKSYNC  16  /* 1: block-synchronous bounces, the live rays of each 1024-path block
                                   compacted before every closest-hit pass (experimental; nodes must
                                   fit 47 KB of LDS beside the 32 KB exchange), 0 default */
+#define MM_OPT_CHUNK_ORDER 17 /* wave-persistent kernel, frame in one launch: 1 hand out the 64-path chunks
+                                  longest first, by their durations in the previous launch of the same
+                                  tile (LPT order: the cheap chunks run in the launch tail; two small sort
+                                  kernels follow each launch), 0 pixel order (default: chunk durations
+                                  vary too little for LPT to shorten the tail, profiles/r01_ab_chunk_order.txt) */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

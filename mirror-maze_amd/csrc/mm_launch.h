@@ -34,6 +34,11 @@ struct TileJob {
     uint32_t wave_ts_cap = 0;
     uint32_t fair = 0;   // MM_OPT_FAIR bits (wave-persistent kernel scheduling)
     uint32_t grab = 1;   // 64-path chunks claimed per atomic (MM_OPT_GRAB)
+    // MM_OPT_CHUNK_ORDER (wave-persistent kernel): queue position q runs
+    // 64-path chunk order[q] (a permutation; null = identity), and cost[chunk]
+    // receives the chunk's duration in wall_clock64() ticks (null = off).
+    const uint32_t* order = nullptr;
+    uint32_t* cost = nullptr;
 };
 
 struct MegaOpts {
@@ -55,6 +60,11 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
                                     int loop_form, hipStream_t s);
+
+// Longest-first chunk order from the previous launch's chunk durations
+// (chunk_order.hip): order = chunks sorted by descending duration in
+// 1/16-octave bins (ties in any order).  tmp: 1024 u32 of scratch, zeroed here.
+hipError_t launch_chunk_order(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* tmp, hipStream_t s);
 
 // Throughput mode, block-synchronous bounces with ray compaction
 // (trace_block.hip, MM_OPT_BLOCKSYNC): 1024-thread blocks, BVH in LDS.

@@ -93,6 +93,15 @@ struct mm_ctx {
     uint32_t opt_fair = 0;       // MM_OPT_FAIR: issue priority for waves behind the mean chunk count
     uint32_t opt_grab = 1;       // chunks per work-counter atomic
     bool opt_blocksync = false;  // block-synchronous bounces with ray compaction (trace_block.hip)
+    uint32_t opt_chunk_order = 0;  // MM_OPT_CHUNK_ORDER: 0 pixel order, 1 longest first (previous launch)
+    // longest-first chunk order (chunk_order.hip): durations of the last launch
+    // of the tile `order_key` describes, the permutation sorted from them
+    uint32_t* d_cost = nullptr;
+    uint32_t* d_order = nullptr;
+    uint32_t* d_order_tmp = nullptr;   // 1024 u32: histogram + cursors
+    size_t cost_cap = 0, order_cap = 0, order_tmp_cap = 0;
+    uint32_t order_key[8] = {};
+    bool order_ready = false;
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
@@ -295,6 +304,7 @@ void mm_destroy(mm_ctx* c) {
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave);
+    (void)hipFree(c->d_cost); (void)hipFree(c->d_order); (void)hipFree(c->d_order_tmp);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -355,6 +365,11 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
         case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
         case MM_OPT_BLOCKSYNC: c->opt_blocksync = value != 0; return MM_OK;
+        case MM_OPT_CHUNK_ORDER:
+            if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "chunk order must be 0 or 1");
+            c->opt_chunk_order = (uint32_t)value;
+            c->order_ready = false;
+            return MM_OK;
         case MM_OPT_GRAB:
             if (value < 1 || value > 16) return fail(c, MM_ERR_INVALID, "grab must be 1..16");
             c->opt_grab = (uint32_t)value;
@@ -651,6 +666,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         job.grab = c->opt_grab;
         job.wave_ts_cap = c->wave_ts_cap;
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
+        uint32_t sort_chunks = 0;  // > 0: queue the longest-first sort of this launch's chunk durations
         if (c->opt_tail_gate) HIPC(c, launch_tail_gate(c->stream));
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
@@ -732,10 +748,27 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             if (c->opt_ww < 0 && ww == 5 && lean_fits && mode != 6) ww = 7;
             if ((ww == 7 || ww == 9) && !lean_fits) ww = 5;
             if (ww == 9) sc.nodes = c->d_nodes_cons;  // the search's expanded boxes (LDS and global)
+            // longest-first chunk order: queue the previous launch's sort for a tile of the same
+            // geometry (a frame that is one launch), record this launch's chunk durations
+            const uint32_t n_chunks = (job.w * job.h * job.e.spp + 63u) / 64u;
+            const bool ordered = c->opt_chunk_order && ww != 4 && ww != 6 && rows_per_batch >= h;
+            if (ordered) {
+                const uint32_t key[8] = {job.x0, job.y0, job.w, job.h, job.y_stride, job.view_w, job.e.spp, 1u};
+                if (!std::equal(key, key + 8, c->order_key)) {
+                    std::copy(key, key + 8, c->order_key);
+                    c->order_ready = false;
+                }
+                if ((rc = ensure(c, c->d_cost, c->cost_cap, n_chunks))) return rc;
+                if ((rc = ensure(c, c->d_order, c->order_cap, n_chunks))) return rc;
+                if ((rc = ensure(c, c->d_order_tmp, c->order_tmp_cap, 1024))) return rc;
+                job.order = c->order_ready ? c->d_order : nullptr;
+                job.cost = c->d_cost;
+            }
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, slots,
                                              block, c->opt_min_waves, ww, c->stream));
+            sort_chunks = ordered ? n_chunks : 0u;
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
             PersistOpts po;
             po.block = c->opt_block ? c->opt_block : 1024u;
@@ -759,6 +792,11 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
                                       reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
         }
         if ((rc = prof_mark(c))) return rc;
+        if (sort_chunks) {  // after the trace kernel's event pair: the sort is not trace time
+            HIPC(c, launch_chunk_order(c->d_cost, sort_chunks, c->d_order, c->d_order_tmp, c->stream));
+            c->order_ready = true;
+            launches += 2;
+        }
         if (fuse) {
             launches += 1;
             continue;

@@ -171,7 +171,12 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
                 __builtin_amdgcn_s_setprio(0);
         }
         ++chunks;
-        const uint32_t path = base + lane;
+        // MM_OPT_CHUNK_ORDER: queue position -> chunk through the cost-sorted
+        // permutation (paths are keyed by pixel/sample, so any order gives the
+        // same samples); the chunk's duration is recorded for the next sort
+        const uint32_t chunk = job.order ? __builtin_amdgcn_readfirstlane(job.order[base >> 6]) : (base >> 6);
+        const unsigned long long t_chunk = job.cost ? (unsigned long long)wall_clock64() : 0ull;
+        const uint32_t path = chunk * 64u + lane;
         const bool valid = path < n_paths;
         F3 s = F3{0.0f, 0.0f, 0.0f};
         if (valid) {
@@ -188,6 +193,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
             paths++;
         }
         if (job.fuse) resolve_in_wave(job, s, path, valid);
+        if (job.cost && lane == 0) job.cost[chunk] = (uint32_t)((unsigned long long)wall_clock64() - t_chunk);
     }
     if (kStats) flush_stats(stats, c, paths);
     return chunks;

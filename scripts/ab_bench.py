@@ -69,6 +69,7 @@ VARIANTS["li-b768-w6"] = dict(pipe=1, persist=2, lds=1, block=768, mw=6, ls=0, l
 VARIANTS["brli-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0, lr=1, ww=6)
 VARIANTS["blocksync"] = dict(pipe=1, bsync=1)
 VARIANTS["lean7"] = dict(pipe=1, ww=7)
+VARIANTS["order1"] = dict(pipe=1, order=1)
 VARIANTS["cons9"] = dict(pipe=1, ww=9)
 VARIANTS["li-ldsstack-grec"] = dict(pipe=1, ls=2)
 VARIANTS["li-ldsstack"] = dict(pipe=1, ls=1, lr=0)
@@ -96,6 +97,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--ranks", type=int, default=1, help="trace rank 0's rows of an N-way split (0, N, 2N, ...)")
     ap.add_argument("variants", nargs="*", default=["ref", "mega-global", "mega-lds"])
     a = ap.parse_args()
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
@@ -124,6 +126,8 @@ def main():
             r.set_option(16, v["bsync"])
         if "grab" in v:
             r.set_option(15, v["grab"])
+        if "order" in v:
+            r.set_option(17, v["order"])
         if "fair" in v:
             r.set_option(14, v["fair"])
         if "fuse" in v:
@@ -140,14 +144,16 @@ def main():
             r.set_option(9, v["split"])
         if "th" in v:
             r.set_option(MM_OPT_THRESHOLD, v["th"])
-        out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-        _, st = r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, H, out=out, stats=True)  # warm
+        h = (H + a.ranks - 1) // a.ranks
+        out = torch.zeros((h, W, 4), dtype=torch.float32, device="cuda")
+        _, st = r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, h, y_stride=a.ranks, out=out,
+                             stats=True)  # warm
         torch.cuda.synchronize()
         r.set_profiling(True)
         r.kernel_timing(reset=True)
         t0 = time.perf_counter()
-        for f in range(a.frames):
-            r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, H, out=out)
+        for f in range(a.frames):  # frames 1.. (the per-frame RNG differs from the warm frame's)
+            r.trace_tile(u, make_ext(spp, bl, ml, frame=f + 1), 0, 0, W, h, y_stride=a.ranks, out=out)
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / a.frames * 1e3
         kms, kn = r.kernel_timing(reset=True)

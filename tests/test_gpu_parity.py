@@ -139,6 +139,8 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "leafinterior-grab3-fair": (1, {1: 1, 3: 2, 7: 5, 15: 3, 14: 1}),
     "blocksync": (1, {3: 2, 16: 1}),
     "leanli": (1, {3: 2, 7: 7}),
+    "leanli-order": (1, {3: 2, 7: 7, 17: 1}),
+    "leafinterior-order-grab2": (1, {3: 2, 7: 5, 17: 1, 15: 2}),
     "cons": (1, {3: 2, 7: 9}),
     "cons-split2kb": (1, {3: 2, 7: 9, 9: 2}),
     "cons-globalrects": (1, {3: 2, 7: 9, 8: 0, 11: 1}),
@@ -190,7 +192,8 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
 @pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
                                   "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
                                   "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
-                                  "leafinterior-grab3-fair", "blocksync", "leanli", "cons"])
+                                  "leafinterior-grab3-fair", "blocksync", "leanli", "cons", "leanli-order",
+                                  "leafinterior-order-grab2"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -237,6 +240,37 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert st.rays >= st.paths  # at least one query per path
     img = full.cpu().numpy()
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
+
+
+def test_chunk_order_bit_identical(gpu):
+    """MM_OPT_CHUNK_ORDER: chunks handed out longest first (by the previous
+    launch's durations) give the same frames and the same work counts as pixel
+    order -- C3 over several frames, a row-split tile of another geometry in
+    between (the order is keyed on the tile), and an accumulated frame."""
+    import torch
+
+    from mirror_maze import MM_EXT_ACCUMULATE, Renderer, default_uniform, make_ext
+
+    s = _scene(32)
+    base, lpt = Renderer(0), Renderer(0)
+    lpt.set_option(17, 1)
+    for r in (base, lpt):
+        r.upload_scene(s)
+    u = default_uniform(1920, 1080, 0)
+    plan = [(0, 0, 1080, 1), (1, 0, 1080, 1), (2, 0, 1080, 1), (3, 1, 540, 2), (4, 1, 540, 2), (5, 0, 1080, 1),
+            (6, 0, 1080, 1)]
+    for frame, y0, h, stride in plan:
+        e = make_ext(8, 8, 8, frame=frame)
+        a, sa = base.trace_tile(u, e, 0, y0, 1920, h, y_stride=stride, stats=True)
+        b, sb = lpt.trace_tile(u, e, 0, y0, 1920, h, y_stride=stride, stats=True)
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), frame
+        assert (sa.rays, sa.node_visits, sa.rect_tests, sa.paths) == (sb.rays, sb.node_visits, sb.rect_tests, sb.paths)
+    e = make_ext(8, 8, 8, frame=7, flags=MM_EXT_ACCUMULATE)
+    base.trace_tile(u, e, 0, 0, 1920, 1080, out=a)
+    lpt.trace_tile(u, e, 0, 0, 1920, 1080, out=b)
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    base.close()
+    lpt.close()
 
 
 def test_c4_eight_way_row_split_invariance(ren, gpu):
