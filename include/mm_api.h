@@ -173,9 +173,6 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   tile (LPT order: the cheap chunks run in the launch tail; two small sort
                                   kernels follow each launch), 0 pixel order (default: chunk durations
                                   vary too little for LPT to shorten the tail, profiles/r01_ab_chunk_order.txt) */
-#define MM_OPT_TAIL_SPLIT 18  /* wave-persistent kernel, fused resolve, loop form 7 or 5: 1 once the chunk
-                                  queue is empty, waves without work take over paths that busy waves hand
-                                  over at bounce boundaries (shortens the launch tail), 0 off (default) */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64
@@ -183,12 +180,6 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
  * done, exit time (wall_clock64 ticks, 100 MHz) and the number of 64-path
  * chunks it traced.  NULL turns it off (default).  scripts/timeline_probe.py */
 int  mm_set_wave_timeline(mm_ctx* ctx, unsigned long long* dev_buf, uint32_t n_waves);
-
-/* Diagnostics of the last MM_OPT_TAIL_SPLIT launch: copies up to n of its
- * control words (trace_kernels.hip: kIdle 0, kDone 32, kHead 64, kTaken 65,
- * kSlots 96, kTakers 128; 160 + 14/15/17 = wall_clock64 when the queue ran
- * dry / of the last wave's exit / at launch, 160 + 16 = paths completed). */
-int  mm_tail_counters(mm_ctx* ctx, uint32_t* out, uint32_t n);
 
 /* Wait for all work queued by this context. */
 int  mm_sync(mm_ctx* ctx);

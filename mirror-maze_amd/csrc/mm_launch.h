@@ -17,26 +17,6 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
                                uint32_t grid_w, uint32_t grid_h, float4* fb, uint32_t* fb8,
                                unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
 
-// MM_OPT_TAIL_SPLIT buffers (wave-persistent kernel, loop forms 11/12): once
-// the chunk queue is empty, waves without work take paths that busy waves
-// hand over at bounce boundaries (trace_kernels.hip, tailsplit_body).
-//   ctl: idle waves, paths completed, ring entries reserved / claimed, slots
-//   allocated, taker tickets -- one 128-B line each (trace_kernels.hip kIdle..);
-//   zeroed per launch with slot_done
-//   ring[e]   4 float4: (ori, seed) (dir, n) (T, mh) (L, ident = slot << 6 | lane)
-//   ready[e]  == epoch once ring[e] is written (epoch > 0 differs per launch)
-//   slot_meta[slot] (first path of the chunk, valid paths), slot_done[slot]
-//   paths of the chunk committed, staging[slot * 64 + lane] their samples
-struct TailCtl {
-    uint32_t* ctl = nullptr;
-    uint32_t* slot_done = nullptr;
-    uint2* slot_meta = nullptr;
-    float4* staging = nullptr;
-    float4* ring = nullptr;
-    uint32_t* ready = nullptr;
-    uint32_t ring_cap = 0, slot_cap = 0, epoch = 0;
-};
-
 struct TileJob {
     mm_uniform u;
     mm_ext e;
@@ -59,7 +39,6 @@ struct TileJob {
     // receives the chunk's duration in wall_clock64() ticks (null = off).
     const uint32_t* order = nullptr;
     uint32_t* cost = nullptr;
-    TailCtl tail;
 };
 
 struct MegaOpts {

@@ -102,14 +102,6 @@ struct mm_ctx {
     size_t cost_cap = 0, order_cap = 0, order_tmp_cap = 0;
     uint32_t order_key[8] = {};
     bool order_ready = false;
-    uint32_t opt_tail_split = 0;   // MM_OPT_TAIL_SPLIT: idle waves take paths busy waves hand over
-    // tail split buffers (TailCtl): ctl + slot_done (zeroed per launch), slot_meta, staging, ring, ready
-    uint32_t* d_tail_ctl = nullptr;
-    uint2* d_slot_meta = nullptr;
-    float4* d_staging = nullptr;
-    float4* d_ring = nullptr;
-    uint32_t* d_ready = nullptr;
-    uint32_t tail_epoch = 0;
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
@@ -257,31 +249,6 @@ int prof_mark(mm_ctx* c) {
     return MM_OK;
 }
 
-// Tail split buffers (allocated at first use, kept): slots bound the chunks
-// split per launch (one per resident wave at most: 256 CUs x 32 waves), the
-// ring the paths handed over per launch (a donation that does not fit is not
-// made).
-constexpr uint32_t kTailCtlWords = 192;  // trace_kernels.hip: control words on lines of their own + diagnostics
-constexpr uint32_t kTailSlots = 16384;
-constexpr uint32_t kTailRing = 1u << 20;
-
-// All of it is UNCACHED device memory: the per-XCD L2s are not coherent with
-// each other, and an agent-scope (sc1) load is served by the reader's L2 --
-// measured: a poll of the completion counter kept reading a stale L2 copy for
-// ~190 ms.  Uncached, every access goes to HBM and sees the latest value.
-int tail_buffers(mm_ctx* c) {
-    if (c->d_tail_ctl) return MM_OK;
-    const unsigned fl = hipDeviceMallocUncached;
-    HIPC(c, hipExtMallocWithFlags((void**)&c->d_tail_ctl, (kTailCtlWords + kTailSlots) * sizeof(uint32_t), fl));
-    HIPC(c, hipExtMallocWithFlags((void**)&c->d_slot_meta, kTailSlots * sizeof(uint2), fl));
-    HIPC(c, hipExtMallocWithFlags((void**)&c->d_staging, (size_t)kTailSlots * 64 * sizeof(float4), fl));
-    HIPC(c, hipExtMallocWithFlags((void**)&c->d_ring, (size_t)kTailRing * 4 * sizeof(float4), fl));
-    HIPC(c, hipExtMallocWithFlags((void**)&c->d_ready, (size_t)kTailRing * sizeof(uint32_t), fl));
-    HIPC(c, hipMemsetAsync(c->d_ready, 0, (size_t)kTailRing * sizeof(uint32_t), c->stream));
-    c->tail_epoch = 0;
-    return MM_OK;
-}
-
 int read_aux(mm_ctx* c, mm_stats* st) {
     unsigned long long h[5];
     HIPC(c, hipMemcpyAsync(h, c->d_aux, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -289,19 +256,6 @@ int read_aux(mm_ctx* c, mm_stats* st) {
     if (st) { st->rays = h[0]; st->node_visits = h[1]; st->rect_tests = h[2]; st->paths = h[3]; }
     if ((uint32_t)h[4] != 0) {
         HIPC(c, hipMemsetAsync(c->d_aux + 4, 0, sizeof(unsigned long long), c->stream));
-        if ((uint32_t)h[4] & 2u) {
-            uint32_t d[24] = {};
-            if (c->d_tail_ctl) {
-                HIPC(c, hipMemcpyAsync(d, c->d_tail_ctl + 160, sizeof(d), hipMemcpyDeviceToHost, c->stream));
-                HIPC(c, hipStreamSynchronize(c->stream));
-            }
-            char msg[512];
-            snprintf(msg, sizeof msg, "tail split: hand-over timed out (internal error): idle %u done %u reserved %u "
-                     "claimed %u slots %u paths %u (queue open %u, chunks %u); ready-spin timeouts %u (entry %u "
-                     "flag %u epoch %u), torn entries %u, timed-out waves %u, flags written %u", d[0], d[1], d[2], d[3],
-                     d[4], d[5], d[6], d[7], d[8], d[9], d[10], c->tail_epoch, d[11], d[12], d[13]);
-            return fail(c, MM_ERR_HIP, msg);
-        }
         return fail(c, MM_ERR_STACK, "traversal stack overflow (depth > 50)");
     }
     return MM_OK;
@@ -351,8 +305,6 @@ void mm_destroy(mm_ctx* c) {
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave);
     (void)hipFree(c->d_cost); (void)hipFree(c->d_order); (void)hipFree(c->d_order_tmp);
-    (void)hipFree(c->d_tail_ctl); (void)hipFree(c->d_slot_meta); (void)hipFree(c->d_staging);
-    (void)hipFree(c->d_ring); (void)hipFree(c->d_ready);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -413,10 +365,6 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
         case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
         case MM_OPT_BLOCKSYNC: c->opt_blocksync = value != 0; return MM_OK;
-        case MM_OPT_TAIL_SPLIT:
-            if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "tail split must be 0 or 1");
-            c->opt_tail_split = (uint32_t)value;
-            return MM_OK;
         case MM_OPT_CHUNK_ORDER:
             if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "chunk order must be 0 or 1");
             c->opt_chunk_order = (uint32_t)value;
@@ -800,28 +748,10 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
             if (c->opt_ww < 0 && ww == 5 && lean_fits && mode != 6) ww = 7;
             if ((ww == 7 || ww == 9) && !lean_fits) ww = 5;
             if (ww == 9) sc.nodes = c->d_nodes_cons;  // the search's expanded boxes (LDS and global)
-            // tail split: forms 7 / 5 with hand-overs to idle waves (fused resolve only)
-            if (c->opt_tail_split && fuse && block == 1024 && c->opt_min_waves == 8 &&
-                ((ww == 7 && (mode == 3 || mode == 7)) || (ww == 5 && (mode == 3 || mode == 6)))) {
-                ww = ww == 7 ? 11 : 12;
-                if ((rc = tail_buffers(c))) return rc;
-                if (++c->tail_epoch == 0) c->tail_epoch = 1;
-                HIPC(c, hipMemsetAsync(c->d_tail_ctl, 0, (kTailCtlWords + kTailSlots) * sizeof(uint32_t),
-                                       c->stream));
-                job.tail.ctl = c->d_tail_ctl;
-                job.tail.slot_done = c->d_tail_ctl + kTailCtlWords;
-                job.tail.slot_meta = c->d_slot_meta;
-                job.tail.staging = c->d_staging;
-                job.tail.ring = c->d_ring;
-                job.tail.ready = c->d_ready;
-                job.tail.ring_cap = kTailRing;
-                job.tail.slot_cap = kTailSlots;
-                job.tail.epoch = c->tail_epoch;
-            }
             // longest-first chunk order: queue the previous launch's sort for a tile of the same
             // geometry (a frame that is one launch), record this launch's chunk durations
             const uint32_t n_chunks = (job.w * job.h * job.e.spp + 63u) / 64u;
-            const bool ordered = c->opt_chunk_order && ww != 4 && ww != 6 && ww < 11 && rows_per_batch >= h;
+            const bool ordered = c->opt_chunk_order && ww != 4 && ww != 6 && rows_per_batch >= h;
             if (ordered) {
                 const uint32_t key[8] = {job.x0, job.y0, job.w, job.h, job.y_stride, job.view_w, job.e.spp, 1u};
                 if (!std::equal(key, key + 8, c->order_key)) {
@@ -884,16 +814,6 @@ int mm_sync(mm_ctx* c) {
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
     return read_aux(c, nullptr);
-}
-
-int mm_tail_counters(mm_ctx* c, uint32_t* out, uint32_t n) {
-    if (!c || !out) return MM_ERR_INVALID;
-    if (!c->d_tail_ctl) return fail(c, MM_ERR_INVALID, "mm_tail_counters: no tail-split launch yet");
-    n = std::min(n, kTailCtlWords);
-    HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipMemcpyAsync(out, c->d_tail_ctl, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
-    return MM_OK;
 }
 
 int mm_set_profiling(mm_ctx* c, int enable) {

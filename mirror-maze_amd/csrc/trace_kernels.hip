@@ -284,376 +284,12 @@ __device__ __forceinline__ uint32_t bouncerefill_body(const DevScene& sc, const 
     return 0;
 }
 
-// ---------------------------------------------------------------------------
-// Tail split (MM_OPT_TAIL_SPLIT; loop form 11 = form 7 + split, 12 = form 5 +
-// split).  A launch's tail -- from the first wave that finds the chunk queue
-// empty to the last wave's end -- is ~0.4 ms whatever the order of the chunks
-// (profiles/r01_timeline_probe.txt, r01_ab_chunk_order.txt): every wave is
-// somewhere inside a 64-path chunk whose duration is its longest path's.
-// Here a wave that finds the queue empty registers as idle and takes paths
-// from a ring in HBM; a busy wave, at a bounce boundary while idle waves are
-// waiting, hands over half of its live paths (those with >= 2 bounces left):
-// the path state goes into the ring and the chunk gets a staging slot, into
-// which every path of that chunk then writes its sample; whoever commits the
-// chunk's last path resolves its pixels (resolve_in_wave on the staged
-// samples: the same reduction, so bit-identical).  A path runs the same
-// operations wherever it runs, so samples are bit-identical too.  Release /
-// acquire at agent scope orders the ring entries, slot records and staged
-// samples across XCDs.  Every wave leaves once all paths are committed (and
-// after 2 s of idling at the latest, flagging an error: never expected).
-constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
-// control words, one 128-B line each (pollers of one must not slow the atomics on another)
-constexpr uint32_t kIdle = 0, kDone = 32, kHead = 64, kTaken = 65, kSlots = 96, kTakers = 128, kDiag = 160;
-constexpr unsigned long long kTailTimeoutTicks = 200000000ull;  // 2 s of wall_clock64
-constexpr uint32_t kMinHandOver = 8;  // live paths (>= 2 bounces left) a wave needs to hand half over
-constexpr uint32_t kMaxTakers = 512;  // waves that stay to take paths once the queue is dry; the rest leave
-constexpr uint32_t kIdleRefresh = 1000;  // ticks (10 us) between a block's global reads of the idle count
-__shared__ volatile uint32_t s_tail_idle;   // the block's copy of ctl[kIdle] (loop forms 11 / 12)
-__shared__ volatile uint32_t s_tail_pending;  // ... and of ring entries reserved but not claimed
-__shared__ volatile uint32_t s_tail_stamp;  // wall_clock64 (low 32 bits) of its last refresh
-
-struct SplitState {  // wave-uniform
-    uint32_t slot;     // owner: the chunk's staging slot, kNoSlot until its first hand-over
-    uint32_t base;     // owner: first path of the chunk; taker: first ring entry of the batch
-    uint32_t n_valid;  // owner: valid paths of the chunk
-    bool owner;        // paths from the queue (else taken over from the ring)
-    bool near_end;     // the queue may run dry before this batch ends (< 3 chunks per wave left)
-};
-
-__device__ __forceinline__ uint32_t ld_relaxed(uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_relaxed64(uint32_t* p) {
-    return __hip_atomic_load(reinterpret_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_acquire(uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Hand-over data (ring entries, slot records, staged samples) moves between
-// XCDs, whose L2s are not coherent with each other for ordinary accesses:
-// every word is written and read as an agent-scope atomic (L2 bypassed), so
-// the fences order exactly these accesses.  Only tail traffic goes this way.
-__device__ __forceinline__ void st_word(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_f4(float4* p, float4 v) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(p);
-    st_word(w + 0, __float_as_uint(v.x));
-    st_word(w + 1, __float_as_uint(v.y));
-    st_word(w + 2, __float_as_uint(v.z));
-    st_word(w + 3, __float_as_uint(v.w));
-}
-__device__ __forceinline__ float4 ld_f4(float4* p) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(p);
-    return make_float4(__uint_as_float(ld_relaxed(w + 0)), __uint_as_float(ld_relaxed(w + 1)),
-                       __uint_as_float(ld_relaxed(w + 2)), __uint_as_float(ld_relaxed(w + 3)));
-}
-
-__device__ __forceinline__ uint64_t lanemask_lt_ts() {
-    const uint32_t lane = threadIdx.x & 63u;
-    return lane ? (~0ull >> (64 - lane)) : 0ull;
-}
-
-// A lane's path identity (staging index slot * 64 + lane in chunk): owner
-// waves derive it, taken-over paths read it back from their ring entry (so it
-// needs no register across the bounce loop).
-__device__ __forceinline__ uint32_t path_ident(const TileJob& job, const SplitState& ss) {
-    const uint32_t lane = threadIdx.x & 63u;
-    if (ss.owner) return (ss.slot << 6) | lane;
-    return ld_relaxed(reinterpret_cast<uint32_t*>(job.tail.ring + 4 * (size_t)(ss.base + lane) + 3) + 3);
-}
-
-// At a bounce boundary (all 64 lanes): hand half of the live paths with >= 2
-// bounces left to the ring when idle waves wait and the ring cannot feed them.
-__device__ __forceinline__ void tail_donate(const TileJob& job, PathState& p, bool& live, bool& gave,
-                                            SplitState& ss) {
-    const TailCtl& tc = job.tail;
-    const uint32_t lane = threadIdx.x & 63u;
-    // only queue chunks that may still run when the queue is dry hand over (taken-over paths are not
-    // passed on again: every hand-over costs a claim on one contended counter)
-    if (!ss.owner || !ss.near_end) return;
-    // the idle count through the block's LDS copy, refreshed at most every kIdleRefresh ticks: a
-    // global poll per wave and bounce from thousands of waves stalls every access to that line
-    const uint32_t now = (uint32_t)wall_clock64();
-    uint32_t idle, pending;
-    if (now - __builtin_amdgcn_readfirstlane(s_tail_stamp) > kIdleRefresh) {
-        idle = __builtin_amdgcn_readfirstlane(ld_relaxed(tc.ctl + kIdle));
-        const uint64_t ht = ld_relaxed64(tc.ctl + kHead);
-        pending = __builtin_amdgcn_readfirstlane((uint32_t)ht - (uint32_t)(ht >> 32));
-        if (lane == 0) {
-            s_tail_idle = idle;
-            s_tail_pending = pending;
-            s_tail_stamp = now;
-        }
-    } else {
-        idle = __builtin_amdgcn_readfirstlane(s_tail_idle);
-        pending = __builtin_amdgcn_readfirstlane(s_tail_pending);
-    }
-    if (idle == 0 || pending >= 64u * idle) return;  // no taker waiting, or the ring already feeds them
-    const uint64_t m = __ballot(live && p.n + 1 < (int)job.e.bounce_limit + p.mh);
-    const uint32_t cnt = (uint32_t)__popcll(m);
-    if (cnt < kMinHandOver) return;
-    const uint32_t k = cnt / 2;
-    if (ss.owner && ss.slot == kNoSlot) {  // the chunk's staging slot, at its first hand-over
-        uint32_t sl = 0;
-        if (lane == 0) sl = atomicAdd(tc.ctl + kSlots, 1u);
-        sl = __builtin_amdgcn_readfirstlane(sl);
-        if (sl >= tc.slot_cap) return;
-        if (lane == 0) {
-            st_word(reinterpret_cast<uint32_t*>(tc.slot_meta + sl), ss.base);
-            st_word(reinterpret_cast<uint32_t*>(tc.slot_meta + sl) + 1, ss.n_valid);
-        }
-        ss.slot = sl;
-    }
-    // reserve k entries, never past the capacity (a reserved entry is always written)
-    uint32_t h0 = 0xFFFFFFFFu;
-    if (lane == 0) {
-        uint32_t h = ld_relaxed(tc.ctl + kHead);
-        while (h + k <= tc.ring_cap) {
-            const uint32_t prev = atomicCAS(tc.ctl + kHead, h, h + k);
-            if (prev == h) {
-                h0 = h;
-                break;
-            }
-            h = prev;
-        }
-    }
-    h0 = __builtin_amdgcn_readfirstlane(h0);
-    if (h0 == 0xFFFFFFFFu) return;
-    const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt_ts());
-    const bool give = ((m >> lane) & 1ull) && rank >= cnt - k;
-    const uint32_t e = h0 + rank - (cnt - k);
-    if (give) {
-        float4* r = tc.ring + 4 * (size_t)e;
-        st_f4(r + 0, make_float4(p.ori.x, p.ori.y, p.ori.z, __uint_as_float(p.seed)));
-        st_f4(r + 1, make_float4(p.dir.x, p.dir.y, p.dir.z, __int_as_float(p.n)));
-        st_f4(r + 2, make_float4(p.T.x, p.T.y, p.T.z, __int_as_float(p.mh)));
-        st_f4(r + 3, make_float4(p.L.x, p.L.y, p.L.z, __uint_as_float(path_ident(job, ss))));
-    }
-    // publish (write-through payload, so no release fence): drain this wave's stores, then the flags
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (give) {
-        atomicExch(tc.ready + e, tc.epoch);
-        live = false;
-        gave = true;
-        atomicAdd(tc.ctl + kDiag + 13, 1u);  // diagnostics: flags written
-    }
-}
-
-// Commit finished paths of split chunks and taken-over paths (all 64 lanes):
-// stage the samples, count them per chunk, and resolve every chunk whose last
-// path this wave committed.
-__device__ __forceinline__ void tail_commit(const TileJob& job, F3 s, bool fin, uint32_t ident) {
-    const TailCtl& tc = job.tail;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t slot = ident >> 6;
-    if (fin) st_f4(tc.staging + ident, make_float4(s.x, s.y, s.z, 0.0f));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // write-through samples drained before the counts
-    bool last = false;
-    if (fin) last = atomicAdd(tc.slot_done + slot, 1u) + 1u == ld_relaxed(reinterpret_cast<uint32_t*>(tc.slot_meta + slot) + 1);
-    const uint64_t fm = __ballot(fin);
-    if (lane == 0 && fm) {
-        const uint32_t nf = (uint32_t)__popcll(fm);
-        if (atomicAdd(tc.ctl + kDone, nf) + nf == job.w * job.h * job.e.spp)
-            tc.ctl[kDiag + 18] = (uint32_t)wall_clock64();  // diagnostics: all paths done
-    }
-    uint64_t lm = __ballot(last);
-    if (lm) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other committers' samples
-    while (lm) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(lm);
-        const uint32_t sl = __builtin_amdgcn_readlane(slot, l);
-        const uint2 meta = make_uint2(ld_relaxed(reinterpret_cast<uint32_t*>(tc.slot_meta + sl)),
-                                      ld_relaxed(reinterpret_cast<uint32_t*>(tc.slot_meta + sl) + 1));
-        const bool val = lane < meta.y;
-        const float4 x = val ? ld_f4(tc.staging + (size_t)sl * 64 + lane) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        resolve_in_wave(job, F3{x.x, x.y, x.z}, meta.x + lane, val);
-        lm &= lm - 1;
-    }
-}
-
-// One loop over work batches -- a chunk from the queue, or once it is empty a
-// batch of up to 64 taken-over paths -- sharing one copy of the bounce loop.
-template <bool kStats, int kTrav, typename V, typename Stack>
-__device__ __forceinline__ uint32_t tailsplit_body(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
-                                                   unsigned long long* stats, uint32_t* err, uint32_t* work) {
-    const TailCtl& tc = job.tail;
-    const uint32_t spp = job.e.spp;
-    const uint32_t n_paths = job.w * job.h * spp;
-    const uint32_t lane = threadIdx.x & 63u;
-    const int bounce_limit = (int)job.e.bounce_limit, mirror_limit = (int)job.e.mirror_limit;
-    Counters c;
-    uint32_t paths = 0, chunks = 0;
-    const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
-    bool queue_open = true, timed_out = false;
-    unsigned long long t_idle = 0;
-    uint32_t backoff = 1;  // idle polling: s_sleep(127) x backoff between empty polls (1..8, ~3.4 us each)
-    for (;;) {
-        SplitState ss{kNoSlot, 0u, 0u, true, true};
-        PathState p;
-        p.ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
-        p.dir = F3{0.0f, 0.0f, 0.0f};
-        p.T = F3{1.0f, 1.0f, 1.0f};
-        p.L = F3{0.0f, 0.0f, 0.0f};
-        p.seed = 0;
-        p.n = 0;
-        p.mh = 0;
-        bool has = false;
-        if (queue_open) {
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(work, 64u);
-            const uint32_t base = __builtin_amdgcn_readfirstlane(b);
-            if (base >= n_paths) {  // queue empty: the first kMaxTakers waves stay to take handed-over paths
-                uint32_t ticket = 0;
-                if (lane == 0) ticket = atomicAdd(tc.ctl + kTakers, 1u);
-                if (lane == 0 && ticket == 0) tc.ctl[kDiag + 14] = (uint32_t)wall_clock64();  // queue dry
-                if (__builtin_amdgcn_readfirstlane(ticket) >= kMaxTakers) break;
-                queue_open = false;
-                if (lane == 0) atomicAdd(tc.ctl + kIdle, 1u);
-                t_idle = (unsigned long long)wall_clock64();
-                continue;
-            }
-            ++chunks;
-            ss.base = base;
-            ss.n_valid = min(64u, n_paths - base);
-            ss.near_end = (n_paths - base) / 64u < 3u * n_waves;
-            const uint32_t path = base + lane;
-            has = path < n_paths;
-            if (has) {
-                const uint32_t pix = path / spp, smp = path - pix * spp;
-                const uint32_t j = pix / job.w, i = pix - j * job.w;
-                const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
-                p.seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
-                p.dir = jitter(primary_dir(job.u, px, py), p.seed);
-            }
-        } else {
-            if ((unsigned long long)wall_clock64() - t_idle > kTailTimeoutTicks) {
-                timed_out = true;
-                break;
-            }
-            uint32_t t = 0, k = 0;
-            if (lane == 0) {
-                const uint64_t ht = ld_relaxed64(tc.ctl + kHead);
-                const uint32_t h = (uint32_t)ht;
-                uint32_t tt = (uint32_t)(ht >> 32);
-                while (tt < h) {
-                    const uint32_t kk = min(64u, h - tt);
-                    const uint32_t prev = atomicCAS(tc.ctl + kTaken, tt, tt + kk);
-                    if (prev == tt) {
-                        t = tt;
-                        k = kk;
-                        break;
-                    }
-                    tt = prev;
-                }
-            }
-            t = __builtin_amdgcn_readfirstlane(t);
-            k = __builtin_amdgcn_readfirstlane(k);
-            if (k == 0) {  // nothing handed over: done, or back off (polls stay off the busy waves' way)
-                if (__builtin_amdgcn_readfirstlane(ld_relaxed(tc.ctl + kDone)) >= n_paths) break;
-                for (uint32_t i = 0; i < backoff; ++i) __builtin_amdgcn_s_sleep(127);
-                backoff = min(2u * backoff, 8u);
-                continue;
-            }
-            backoff = 1;
-            if (lane == 0) atomicSub(tc.ctl + kIdle, 1u);
-            ss.owner = false;
-            ss.base = t;
-            has = lane < k;
-            bool ok_entry = true;
-            if (has) {
-                while (ld_relaxed(tc.ready + t + lane) != tc.epoch) {  // written right after its reservation
-                    if ((unsigned long long)wall_clock64() - t_idle > kTailTimeoutTicks) {
-                        ok_entry = false;
-                        atomicAdd(tc.ctl + kDiag + 8, 1u);  // diagnostics
-                        tc.ctl[kDiag + 9] = t + lane;
-                        tc.ctl[kDiag + 10] = ld_relaxed(tc.ready + t + lane);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                float4* r = tc.ring + 4 * (size_t)(t + lane);
-                const float4 r0 = ld_f4(r + 0), r1 = ld_f4(r + 1), r2 = ld_f4(r + 2), r3 = ld_f4(r + 3);
-                p.ori = F3{r0.x, r0.y, r0.z};
-                p.seed = __float_as_uint(r0.w);
-                p.dir = F3{r1.x, r1.y, r1.z};
-                p.n = __float_as_int(r1.w);
-                p.T = F3{r2.x, r2.y, r2.z};
-                p.mh = __float_as_int(r2.w);
-                p.L = F3{r3.x, r3.y, r3.z};
-                // a handed-over path has >= 1 bounce left; anything else would be a torn entry
-                if (!(p.n >= 0 && p.mh >= 0 && p.mh <= mirror_limit && p.n < bounce_limit + p.mh)) {
-                    ok_entry = false;
-                    atomicAdd(tc.ctl + kDiag + 11, 1u);  // diagnostics
-                }
-            }
-            if (__ballot(has && !ok_entry)) {
-                timed_out = true;
-                break;
-            }
-        }
-        // the bounces (trace_path's loop, one bounce per iteration) with hand-overs
-        bool live = has && p.n < bounce_limit + p.mh, gave = false;
-        while (__ballot(live)) {
-            tail_donate(job, p, live, gave, ss);
-            if (live) {
-                float t = kBig;
-                uint32_t k = 0;
-                const bool ok = closest_hit<kStats, V, Stack, kTrav>(sc, v, p.ori, p.dir, t, k, stack, c);
-                if (kStats) c.rays++;
-                if (!ok) {
-                    atomicOr(err, 1u);
-                    live = false;
-                } else if (!shade_step(sc, p, t, k, mirror_limit)) {
-                    live = false;
-                } else {
-                    p.n++;
-                    live = p.n < bounce_limit + p.mh;
-                }
-            }
-        }
-        const bool fin = has && !gave;
-        const F3 s = fin ? F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))}
-                         : F3{0.0f, 0.0f, 0.0f};
-        if (fin) paths++;
-        if (ss.owner && ss.slot == kNoSlot) {
-            resolve_in_wave(job, s, ss.base + lane, has);
-            if (lane == 0 && atomicAdd(tc.ctl + kDone, ss.n_valid) + ss.n_valid == n_paths)
-                tc.ctl[kDiag + 18] = (uint32_t)wall_clock64();  // diagnostics: all paths done
-        } else {
-            tail_commit(job, s, fin, fin ? path_ident(job, ss) : 0u);
-        }
-        if (!ss.owner && lane == 0) atomicAdd(tc.ctl + kIdle, 1u);
-    }
-    if (lane == 0) {  // diagnostics (mm_tail_counters): last exit, batches taken
-        atomicMax(tc.ctl + kDiag + 15, (uint32_t)wall_clock64());
-        atomicAdd(tc.ctl + kDiag + 16, paths);
-    }
-    if (timed_out && lane == 0) {
-        atomicOr(err, 2u);
-        // diagnostics for the error message: counters as this wave saw them
-        tc.ctl[kDiag + 0] = ld_relaxed(tc.ctl + kIdle);
-        tc.ctl[kDiag + 1] = ld_relaxed(tc.ctl + kDone);
-        tc.ctl[kDiag + 2] = ld_relaxed(tc.ctl + kHead);
-        tc.ctl[kDiag + 3] = ld_relaxed(tc.ctl + kTaken);
-        tc.ctl[kDiag + 4] = ld_relaxed(tc.ctl + kSlots);
-        tc.ctl[kDiag + 5] = n_paths;
-        tc.ctl[kDiag + 6] = queue_open ? 1u : 0u;
-        tc.ctl[kDiag + 7] = chunks;
-        atomicAdd(tc.ctl + kDiag + 12, 1u);
-    }
-    if (kStats) flush_stats(stats, c, paths);
-    return chunks;
-}
-
 template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
 __device__ __forceinline__ uint32_t wp_dispatch(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
                                                 float4* __restrict__ samples, unsigned long long* stats,
                                                 uint32_t* err, uint32_t* work, const Cold& cold = Cold{}) {
     if constexpr (kWW == 4) return bouncerefill_body<kStats>(sc, v, stack, job, samples, stats, err, work);
     else if constexpr (kWW == 6) return bouncerefill_body<kStats, V, Stack, 5>(sc, v, stack, job, samples, stats, err, work);
-    else if constexpr (kWW == 11) return tailsplit_body<kStats, 7>(sc, v, stack, job, stats, err, work);
-    else if constexpr (kWW == 12) return tailsplit_body<kStats, 5>(sc, v, stack, job, stats, err, work);
     else return wavepersist_body<kStats, kWW>(sc, v, stack, job, samples, stats, err, work, cold);
 }
 
@@ -685,14 +321,6 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
                                                                          uint32_t* work, uint32_t stack_slots) {
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
     uint32_t chunks = 0;
-    if constexpr (kWW == 11 || kWW == 12) {  // before the staging barrier below
-        if (threadIdx.x == 0) {
-            s_tail_idle = 0;
-            s_tail_pending = 0;
-            s_tail_stamp = (uint32_t)wall_clock64();
-            if (blockIdx.x == 0) job.tail.ctl[160 + 17] = s_tail_stamp;  // diagnostics: launch start
-        }
-    }
     if constexpr (kLds == 4 || kLds == 6) {
         extern __shared__ float4 lds_top[];
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds_top[i] = sc.nodes[i];
@@ -817,8 +445,6 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
     }
     if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
     if (block == 1024 && min_waves == 8 && loop_form == 7) { MM_WP2(3, 1024, 8, 7) MM_WP2(6, 1024, 8, 7) MM_WP2(7, 1024, 8, 7) }
-    if (block == 1024 && min_waves == 8 && loop_form == 11) { MM_WP2(3, 1024, 8, 11) MM_WP2(7, 1024, 8, 11) }
-    if (block == 1024 && min_waves == 8 && loop_form == 12) { MM_WP2(3, 1024, 8, 12) MM_WP2(6, 1024, 8, 12) }
     if (block == 1024 && min_waves == 8 && loop_form == 9) { MM_WP2(3, 1024, 8, 9) MM_WP2(6, 1024, 8, 9) MM_WP2(7, 1024, 8, 9) }
     // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS
     if (block == 768 && min_waves == 6 && loop_form == 5) { MM_WP2(3, 768, 6, 5) MM_WP2(6, 768, 6, 5) }

@@ -70,8 +70,6 @@ VARIANTS["brli-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0,
 VARIANTS["blocksync"] = dict(pipe=1, bsync=1)
 VARIANTS["lean7"] = dict(pipe=1, ww=7)
 VARIANTS["order1"] = dict(pipe=1, order=1)
-VARIANTS["split"] = dict(pipe=1, tsplit=1)
-VARIANTS["li-split"] = dict(pipe=1, tsplit=1, ww=5)
 VARIANTS["cons9"] = dict(pipe=1, ww=9)
 VARIANTS["li-ldsstack-grec"] = dict(pipe=1, ls=2)
 VARIANTS["li-ldsstack"] = dict(pipe=1, ls=1, lr=0)
@@ -128,8 +126,6 @@ def main():
             r.set_option(16, v["bsync"])
         if "grab" in v:
             r.set_option(15, v["grab"])
-        if "tsplit" in v:
-            r.set_option(18, v["tsplit"])
         if "order" in v:
             r.set_option(17, v["order"])
         if "fair" in v:

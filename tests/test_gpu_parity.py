@@ -140,10 +140,6 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "blocksync": (1, {3: 2, 16: 1}),
     "leanli": (1, {3: 2, 7: 7}),
     "leanli-order": (1, {3: 2, 7: 7, 17: 1}),
-    "leanli-tailsplit": (1, {3: 2, 7: 7, 18: 1}),
-    "leanli-globalrects-tailsplit": (1, {3: 2, 7: 7, 8: 0, 11: 1, 18: 1}),
-    "leafinterior-tailsplit": (1, {3: 2, 7: 5, 18: 1}),
-    "leafinterior-split2kb-tailsplit": (1, {3: 2, 7: 5, 9: 2, 18: 1}),
     "leafinterior-order-grab2": (1, {3: 2, 7: 5, 17: 1, 15: 2}),
     "cons": (1, {3: 2, 7: 9}),
     "cons-split2kb": (1, {3: 2, 7: 9, 9: 2}),
@@ -197,7 +193,7 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
                                   "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
                                   "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
                                   "leafinterior-grab3-fair", "blocksync", "leanli", "cons", "leanli-order",
-                                  "leafinterior-order-grab2", "leanli-tailsplit", "leafinterior-split2kb-tailsplit"])
+                                  "leafinterior-order-grab2"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -275,41 +271,6 @@ def test_chunk_order_bit_identical(gpu):
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     base.close()
     lpt.close()
-
-
-@pytest.mark.parametrize("opts", [{}, {9: 2}])
-def test_tail_split_bit_identical(gpu, opts):
-    """MM_OPT_TAIL_SPLIT: paths handed over to idle waves at bounce boundaries
-    (ring in HBM, staged samples, resolve by the chunk's last committer) give
-    the same C3 frames, accumulated frame and work counts as the default
-    kernel -- whole frames and the 8-way row split (a short launch, so most of
-    it is tail); with the split node cache too (loop form 12)."""
-    import torch
-
-    from mirror_maze import MM_EXT_ACCUMULATE, Renderer, default_uniform, make_ext
-
-    s = _scene(32)
-    base, split = Renderer(0), Renderer(0)
-    split.set_option(18, 1)
-    for k, v in opts.items():
-        base.set_option(k, v)
-        split.set_option(k, v)
-    for r in (base, split):
-        r.upload_scene(s)
-    u = default_uniform(1920, 1080, 0)
-    plan = [(0, 0, 1080, 1), (1, 0, 1080, 1), (2, 3, 135, 8), (3, 7, 135, 8), (4, 0, 1080, 1)]
-    for frame, y0, h, stride in plan:
-        e = make_ext(8, 8, 8, frame=frame)
-        a, sa = base.trace_tile(u, e, 0, y0, 1920, h, y_stride=stride, stats=True)
-        b, sb = split.trace_tile(u, e, 0, y0, 1920, h, y_stride=stride, stats=True)
-        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), frame
-        assert (sa.rays, sa.node_visits, sa.rect_tests, sa.paths) == (sb.rays, sb.node_visits, sb.rect_tests, sb.paths)
-    e = make_ext(8, 8, 8, frame=5, flags=MM_EXT_ACCUMULATE)
-    base.trace_tile(u, e, 0, 0, 1920, 1080, out=a)
-    split.trace_tile(u, e, 0, 0, 1920, 1080, out=b)
-    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
-    base.close()
-    split.close()
 
 
 def test_c4_eight_way_row_split_invariance(ren, gpu):
