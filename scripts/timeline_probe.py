@@ -63,6 +63,13 @@ def main():
                   f"{ext.max():7.1f}  tail {span - ext.min():6.1f} ({(span - ext.min()) / span:.1%})  "
                   f"chunks/wave {ch.mean():.2f} [{ch.min()}-{ch.max()}]  wave-busy {busy / (len(t) * span):.1%}",
                   flush=True)
+            # what balancing the last chunks' paths inside each block could reach: a block's waves
+            # finish together at their mean exit (blocks = consecutive 16-wave groups by wave id)
+            wid = np.nonzero(ts.cpu().numpy()[:, 2] > 0)[0]
+            blk = wid // 16
+            bmean = np.array([ext[blk == b].mean() for b in np.unique(blk)])
+            print(f"    block-balanced bound: last block mean exit {bmean.max():7.1f} (vs last wave {span:7.1f}); "
+                  f"chip mean exit {ext.mean():7.1f}", flush=True)
     r.close()
 
 
