@@ -57,6 +57,11 @@ def parse():
     p.add_argument("--contexts", type=int, default=0,
                    help="renderer contexts (one stream each) that consecutive frames alternate over; "
                         "0 = 1 on one GPU, 2 when the frame is split over ranks")
+    p.add_argument("--batch", type=int, default=8,
+                   help="frames per launch (mm_trace_tile_frames: the frames share one work queue, so the "
+                        "~0.4 ms launch tail is paid once per launch, not per frame); 1 = one frame per launch "
+                        "(then --contexts applies); 0 = time 1 context / 2 contexts / batches of 8 after warmup "
+                        "and keep the fastest")
     p.add_argument("--accumulate", action="store_true",
                    help="temporal accumulation (C5): every frame adds into one running sum per rank "
                         "(MM_EXT_ACCUMULATE) and the frame is gathered once, after the last step")
@@ -147,14 +152,16 @@ def main():
 
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[args.config]
     scene = Scene.build(maze_n, 0)
-    # Frames can alternate over two renderer contexts, each on its own library
-    # stream: frames are independent, so frame k+1's blocks fill the CUs that
-    # frame k's last waves leave idle -- the ~0.4 ms per-launch tail that
-    # bounds strong scaling (profiles/r01_timeline_probe.txt).  Two frames
-    # sharing the GPU also run ~7 % slower (profiles/r01_overlap_probe.txt), so
-    # overlap only pays on short per-rank frames: --contexts 0 (default)
-    # measures both issue modes after warmup and keeps the faster.
-    n_ctx = 1 if args.accumulate else (args.contexts if args.contexts > 0 else 2)
+    # Issue modes.  Every launch ends in a ~0.4 ms tail in which the last waves
+    # finish their last chunks (profiles/r01_timeline_probe.txt) -- 4 % of a
+    # C3 frame, 25 % of a rank's frame at N = 8.  Default (--batch 8): frames
+    # are independent, so up to 8 consecutive frames share ONE launch's work
+    # queue (mm_trace_tile_frames) and the tail is paid once per launch.
+    # --batch 1: one frame per launch, optionally alternating over two
+    # renderer contexts on their own streams so frame k+1's blocks fill the
+    # CUs frame k's tail leaves idle (two frames sharing the GPU run ~7 %
+    # slower, profiles/r01_overlap_probe.txt; --contexts 0 times both).
+    n_ctx = 1 if args.accumulate or args.batch > 1 else (args.contexts if args.contexts > 0 else 2)
     rens = []
     for _ in range(n_ctx):
         r = Renderer(local)
@@ -182,6 +189,9 @@ def main():
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in rens]
     last = [0]
     active = [len(rens)]  # contexts the frames alternate over
+    batch = [1]           # frames per launch (mm_trace_tile_frames), single context
+    fb_max = 1 if args.accumulate else (args.batch if args.batch > 0 else 8)
+    batch_buf = torch.zeros((fb_max, my_rows, W, 4), dtype=torch.float32, device=dev) if fb_max > 1 else None
     progress_t = [time.perf_counter()]
 
     def progress(msg):
@@ -210,6 +220,35 @@ def main():
         last[0] = slot
         return st
 
+    def step_batch(k, frame, n, stats=False):
+        """n frames (frame, frame+1, ...) in one launch of context 0; each frame's tile then goes
+        to the gatherer (copied into its rotating tile) or stays in batch_buf."""
+        with torch.cuda.stream(streams[0]):
+            _, st = rens[0].trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), n, 0, y0, W, my_rows,
+                                              y_stride=y_stride, out=batch_buf[:n], stats=stats)
+            if gatherer:
+                for f in range(n):
+                    gatherer.tile()[:my_rows].copy_(batch_buf[f])
+                    gatherer.put()
+        last[0] = 0
+        return st
+
+    def run_frames(k0, frame0, count):
+        """count frames starting at frame0 in the current issue mode"""
+        if batch[0] > 1:  # ceil(count / batch) launches of as equal sizes as possible
+            n_launch = -(-count // batch[0])
+            i = 0
+            for j in range(n_launch):
+                n = (count - i) // (n_launch - j)
+                step_batch(k0 + i, frame0 + i, n)
+                i += n
+            if not gatherer and count > 0:  # the last frame, for frame_buf
+                with torch.cuda.stream(streams[0]):
+                    tiles1[0][:my_rows].copy_(batch_buf[n - 1])
+        else:
+            for i in range(count):
+                step(k0 + i, frame0 + i)
+
     def gather_accumulated():
         with torch.cuda.stream(streams[0]):
             if gatherer:
@@ -229,27 +268,36 @@ def main():
         if not gatherer:
             frame_buf.copy_(tiles1[last[0]])
 
-    for i in range(args.warmup):
-        step(i, 10_000 + i)
+    if args.batch > 1 and not args.accumulate:  # warm up the issue mode that is timed
+        batch[0] = fb_max
+        run_frames(0, 10_000, args.warmup)
+    else:
+        for i in range(args.warmup):
+            step(i, 10_000 + i)
     drain()
     calib = None
-    if args.contexts == 0 and not args.accumulate:
+    if args.batch > 1 and not args.accumulate:
+        active[0], batch[0] = 1, fb_max
+    elif (args.batch == 0 or args.contexts == 0) and not args.accumulate:
+        # issue modes: one context, two alternating contexts, one context with batches of frames
+        modes = [("1", 1, 1), ("2", 2, 1)] + ([(f"batch{fb_max}", 1, fb_max)] if args.batch == 0 else [])
         calib = {}
         for rep in range(2):
-            for m in (1, 2):
-                active[0] = m
+            for name, m, fb in modes:
+                active[0], batch[0] = m, fb
                 if distributed:
                     dist.barrier()
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-                for i in range(6):
-                    step(i, 20_000 + 8 * rep + i)
+                run_frames(0, 20_000 + 16 * rep, 8)
                 drain()
                 dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
                 if distributed:
                     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-                calib[m] = min(calib.get(m, 1e9), float(dt.item()) / 6 * 1e3)
-        active[0] = 2 if calib[2] < 0.99 * calib[1] else 1  # overlap only for a clear (>1 %) gain
+                calib[name] = min(calib.get(name, 1e9), float(dt.item()) / 8 * 1e3)
+        # the fastest mode; overlap or batching only for a clear (>1 %) gain over one context
+        best = min(modes, key=lambda md: calib[md[0]])
+        active[0], batch[0] = (best[1], best[2]) if calib[best[0]] < 0.99 * calib["1"] else (1, 1)
     for r in rens[:active[0]]:
         r.set_profiling(True)
         r.kernel_timing(reset=True)
@@ -260,10 +308,13 @@ def main():
     if acc_tile is not None:
         with torch.cuda.stream(streams[0]):
             acc_tile.zero_()
-    for i in range(args.steps):
-        step(i, i)
-        if args.steps > 20 and i % 8 == 7:
-            progress(f"timed frame {i + 1}/{args.steps} queued")
+    if batch[0] > 1:
+        run_frames(0, 0, args.steps)
+    else:
+        for i in range(args.steps):
+            step(i, i)
+            if args.steps > 20 and i % 8 == 7:
+                progress(f"timed frame {i + 1}/{args.steps} queued")
     if acc_tile is not None:
         gather_accumulated()  # C5: one gather of the accumulated frame, inside the timed region
     if gatherer:
@@ -307,8 +358,9 @@ def main():
         achieved = alg_bytes / k_avg_s / 1e9
         traffic = None
         tf = REPO / "profiles" / f"traffic_{args.config}_{args.pipeline}.json"
-        if tf.exists():
-            traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+        if tf.exists() and not args.emulate_ranks:  # measured on one-frame, whole-frame launches: x frames/launch
+            t1 = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+            traffic = None if t1 is None or world > 1 else round(t1 * args.steps / max(k_launches, 1))
         valu_ops = (25 * 2 * (visits / max(k_launches, 1)) + 71 * (rtests / max(k_launches, 1)))
         line = {
             "metric": "Mrays/sec + ms/frame at 1920x1080, 8 spp, 8 bounces; 1/2/4/8-GPU scaling",
@@ -329,6 +381,7 @@ def main():
                        "parallelism": (f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU") +
                                       (f" (emulating rank 0 of {args.emulate_ranks})" if args.emulate_ranks > 1 else ""),
                        "frame_contexts": active[0],
+                       "frames_per_launch": (round(args.steps / max(k_launches, 1), 2) if batch[0] > 1 else 1),
                        "temporal_accumulation": bool(args.accumulate),
                        "options": args.opt or None,
                        "frame_contexts_calibration_ms": ({str(k): round(v, 3) for k, v in calib.items()}

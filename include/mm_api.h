@@ -115,6 +115,19 @@ int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
                    uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
                    uint32_t y_stride, float* out_dev, mm_stats* stats);
 
+/* Several consecutive frames of the same tile in ONE launch: frame f (0 <=
+ * f < n_frames) is traced with RNG frame ext->frame + f into out_dev + f*w*h*4
+ * (out_dev: n_frames*w*h float4, frame-major); each frame is bit-identical to
+ * mm_trace_tile(..., frame = ext->frame + f).  The frames share the launch's
+ * work queue, so the ~0.4 ms tail in which the last waves finish their last
+ * chunks is paid once per launch instead of once per frame (throughput mode
+ * for frame sequences; a frame's result is only complete when the launch is).
+ * Needs the wave-persistent kernel with the fused resolve (64 % spp == 0);
+ * MM_EXT_ACCUMULATE is rejected (frames of one launch run concurrently). */
+int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext, uint32_t n_frames,
+                          uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                          uint32_t y_stride, float* out_dev, mm_stats* stats);
+
 /* Pipeline selection for mm_trace_tile (MM_PIPE_AUTO picks the fastest). */
 #define MM_PIPE_AUTO       0
 #define MM_PIPE_MEGAKERNEL 1   /* one thread per path, bounce loop in-kernel */

@@ -39,6 +39,10 @@ struct TileJob {
     // receives the chunk's duration in wall_clock64() ticks (null = off).
     const uint32_t* order = nullptr;
     uint32_t* cost = nullptr;
+    // Multi-frame launch (mm_trace_tile_frames; wave-persistent kernel, fused
+    // resolve): the queue holds n_frames frames' chunks back to back; frame f
+    // uses RNG frame e.frame + f and writes out + f * w * h.
+    uint32_t n_frames = 1;
 };
 
 struct MegaOpts {

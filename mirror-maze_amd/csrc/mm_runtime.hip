@@ -616,8 +616,10 @@ int mm_read_framebuffer(mm_ctx* c, float* rgba, uint8_t* rgba8) {
     return MM_OK;
 }
 
-int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, uint32_t y0, uint32_t w,
-                  uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
+namespace {
+
+int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_frames, uint32_t x0, uint32_t y0,
+                    uint32_t w, uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
     if (!c) return MM_ERR_INVALID;
     if (!c->has_scene) return fail(c, MM_ERR_NO_SCENE, "mm_trace_tile: no scene uploaded");
     if (!u || !e || !out_dev) return fail(c, MM_ERR_INVALID, "mm_trace_tile: null argument");
@@ -641,6 +643,19 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
     const uint64_t batch_paths = fuse ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
+    if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
+    if (n_frames > 1) {
+        // several frames in one launch: the wave-persistent kernel's queue with the fused resolve
+        if (!fuse || c->opt_blocksync)
+            return fail(c, MM_ERR_UNSUPPORTED, "mm_trace_tile_frames: needs the wave-persistent kernel with the "
+                                               "fused resolve (64 % spp == 0)");
+        if (e->flags & MM_EXT_ACCUMULATE)
+            return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: frames of one launch cannot accumulate into "
+                                           "one image");
+        const uint64_t queue = ((row_paths * h + 63) / 64) * 64 * n_frames;
+        if (rows_per_batch < h || queue + (1ull << 24) > 0xFFFFFFFFull)
+            return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: more paths than one launch holds (2^32)");
+    }
     int rc = fuse ? MM_OK : ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
     if (rc) return rc;
     // aux: [0..3] stats (zeroed only when counted), [4] sticky error flag
@@ -666,6 +681,7 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
         job.grab = c->opt_grab;
         job.wave_ts_cap = c->wave_ts_cap;
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
+        job.n_frames = n_frames;
         uint32_t sort_chunks = 0;  // > 0: queue the longest-first sort of this launch's chunk durations
         if (c->opt_tail_gate) HIPC(c, launch_tail_gate(c->stream));
         if ((rc = prof_mark(c))) return rc;
@@ -807,6 +823,18 @@ int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, 
     if ((rc = end_timing(c, launches))) return rc;
     if (want_stats) return read_aux(c, stats);
     return MM_OK;
+}
+
+}  // namespace
+
+int mm_trace_tile(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t x0, uint32_t y0, uint32_t w,
+                  uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
+    return trace_tile_impl(c, u, e, 1, x0, y0, w, h, y_stride, out_dev, stats);
+}
+
+int mm_trace_tile_frames(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_frames, uint32_t x0,
+                         uint32_t y0, uint32_t w, uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
+    return trace_tile_impl(c, u, e, n_frames, x0, y0, w, h, y_stride, out_dev, stats);
 }
 
 int mm_sync(mm_ctx* c) {

@@ -31,8 +31,10 @@ __device__ __forceinline__ void flush_stats(unsigned long long* stats, const Cou
 // 8 by xor-shuffles (a+b == b+a exactly), blocks added left to right by the
 // pixel's first lane; otherwise a left-to-right sum.  Then / spp -- the same
 // operations in the same order as k_resolve, so the pixel is bit-identical.
-// Called by all 64 lanes (uniform control flow); `valid` lanes' pixels written.
-__device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32_t path, bool valid) {
+// Called by all 64 lanes (uniform control flow); `valid` lanes' pixels written
+// to out (the job's output, or its frame's slice of it in a multi-frame launch).
+__device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32_t path, bool valid,
+                                                float4* __restrict__ out) {
     const uint32_t spp = job.e.spp, lane = threadIdx.x & 63u;
     F3 acc;
     if (spp % 8 == 0) {
@@ -52,10 +54,10 @@ __device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32
         const float m = (float)spp;
         const F3 v = F3{acc.x / m, acc.y / m, acc.z / m};
         if (job.e.flags & MM_EXT_ACCUMULATE) {
-            const float4 o = job.out[pix];
-            job.out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
+            const float4 o = out[pix];
+            out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
         } else {
-            job.out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
+            out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
         }
     }
 }

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(1024, 8) void k_trace_blocksync(DevScene sc, TileJo
         const F3 s = valid ? F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))}
                            : F3{0.0f, 0.0f, 0.0f};
         if (valid) paths++;
-        if (job.fuse) resolve_in_wave(job, s, path, valid);
+        if (job.fuse) resolve_in_wave(job, s, path, valid, job.out);
         else if (valid) samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
         __syncthreads();  // s_base is rewritten by the next fetch
     }

@@ -142,7 +142,9 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
                                                  unsigned long long* stats, uint32_t* err, uint32_t* work,
                                                  const Cold& cold = Cold{}) {
     const uint32_t spp = job.e.spp;
-    const uint32_t n_paths = job.w * job.h * spp;
+    const uint32_t n_paths = job.w * job.h * spp;         // per frame
+    const uint32_t cpf = (n_paths + 63u) / 64u;           // 64-path chunks per frame
+    const uint32_t n_queue = cpf * 64u * job.n_frames;    // the queue, in paths (chunks padded to 64)
     const uint32_t lane = threadIdx.x & 63u;
     const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
     Counters c;
@@ -155,11 +157,11 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
             uint32_t b = 0;
             if (lane == 0) b = atomicAdd(work, grab);
             next = __builtin_amdgcn_readfirstlane(b);
-            end = min(next + grab, n_paths);
+            end = min(next + grab, n_queue);
         }
         const uint32_t base = next;
         next += 64u;
-        if (base >= n_paths) break;
+        if (base >= n_queue) break;
         // MM_OPT_FAIR: a wave behind the mean chunk count runs at raised issue
         // priority (the SIMD arbiter otherwise favours the oldest waves: chunk
         // counts per wave spread 9-59 on C3, 28-37 with this on; the frame time
@@ -174,7 +176,11 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
         // MM_OPT_CHUNK_ORDER: queue position -> chunk through the cost-sorted
         // permutation (paths are keyed by pixel/sample, so any order gives the
         // same samples); the chunk's duration is recorded for the next sort
-        const uint32_t chunk = job.order ? __builtin_amdgcn_readfirstlane(job.order[base >> 6]) : (base >> 6);
+        // queue position -> (frame, chunk of the frame); one frame: frame 0, chunk = position
+        const uint32_t q = base >> 6;
+        const uint32_t fr = job.n_frames > 1 ? q / cpf : 0u;
+        const uint32_t qc = q - fr * cpf;
+        const uint32_t chunk = job.order ? __builtin_amdgcn_readfirstlane(job.order[qc]) : qc;
         const unsigned long long t_chunk = job.cost ? (unsigned long long)wall_clock64() : 0ull;
         const uint32_t path = chunk * 64u + lane;
         const bool valid = path < n_paths;
@@ -183,7 +189,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
             const uint32_t pix = path / spp, smp = path - pix * spp;
             const uint32_t j = pix / job.w, i = pix - j * job.w;
             const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
-            uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
+            uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame + fr);
             const F3 d = jitter(primary_dir(job.u, px, py), seed);
             bool overflow = false;
             s = trace_path<kStats, false, V, Stack, kWW>(sc, v, ori, d, seed, (int)job.e.bounce_limit,
@@ -192,8 +198,9 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
             if (!job.fuse) samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
         }
-        if (job.fuse) resolve_in_wave(job, s, path, valid);
-        if (job.cost && lane == 0) job.cost[chunk] = (uint32_t)((unsigned long long)wall_clock64() - t_chunk);
+        if (job.fuse) resolve_in_wave(job, s, path, valid, job.out + (size_t)fr * job.w * job.h);
+        if (job.cost && lane == 0 && fr == 0)
+            job.cost[chunk] = (uint32_t)((unsigned long long)wall_clock64() - t_chunk);
     }
     if (kStats) flush_stats(stats, c, paths);
     return chunks;

@@ -104,6 +104,8 @@ EXPORTS = {
     "mm_quantize_rgba8": (C.c_int, [P, P, P, C.c_uint64]),
     "mm_trace_tile": (C.c_int, [P, C.POINTER(mm_uniform), C.POINTER(mm_ext), C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_uint32, C.c_uint32, P, C.POINTER(mm_stats)]),
+    "mm_trace_tile_frames": (C.c_int, [P, C.POINTER(mm_uniform), C.POINTER(mm_ext), C.c_uint32, C.c_uint32,
+                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, C.POINTER(mm_stats)]),
     "mm_set_pipeline": (C.c_int, [P, C.c_int]),
     "mm_set_option": (C.c_int, [P, C.c_int, C.c_int]),
     "mm_set_wave_timeline": (C.c_int, [P, P, C.c_uint32]),

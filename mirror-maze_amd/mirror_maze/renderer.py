@@ -158,6 +158,28 @@ class Renderer:
                                         out.data_ptr(), C.byref(st)))
         return out, (st if stats else None)
 
+    def trace_tile_frames(self, uniform: _lib.mm_uniform, ext: _lib.mm_ext, n_frames: int, x0: int, y0: int,
+                          w: int, h: int, y_stride: int = 1, out=None, stats: bool = False):
+        """Render frames ext.frame .. ext.frame + n_frames - 1 of a tile in ONE
+        launch (mm_trace_tile_frames) into a (n_frames, h, w, 4) float32 CUDA
+        tensor (allocated if None); frame f equals trace_tile with frame
+        ext.frame + f.  Returns (out, mm_stats summed over the frames or None)."""
+        import torch
+
+        if out is None:
+            out = torch.zeros((n_frames, h, w, 4), dtype=torch.float32, device=f"cuda:{self.device}")
+        if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()
+                and out.numel() == n_frames * h * w * 4):
+            raise ValueError("out must be a contiguous float32 CUDA tensor of n_frames*h*w*4 elements")
+        if not self._pinned_stream:
+            self._check(lib().mm_set_stream(self._ctx, torch.cuda.current_stream(out.device).cuda_stream))
+        e = _lib.mm_ext(ext.spp, ext.bounce_limit, ext.mirror_limit, ext.frame,
+                        ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0), 0)
+        st = _lib.mm_stats()
+        self._check(lib().mm_trace_tile_frames(self._ctx, C.byref(uniform), C.byref(e), n_frames, x0, y0, w, h,
+                                               y_stride, out.data_ptr(), C.byref(st)))
+        return out, (st if stats else None)
+
     def sync(self) -> None:
         self._check(lib().mm_sync(self._ctx))
 

@@ -273,6 +273,52 @@ def test_chunk_order_bit_identical(gpu):
     lpt.close()
 
 
+@pytest.mark.parametrize("opts", [{}, {9: 2}, {7: 5, 15: 2, 17: 1}])
+def test_multi_frame_launch_bit_identical(gpu, opts):
+    """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
+    F single-frame launches bit for bit, with summed work counts -- C3 whole
+    frames and a row-split tile; the split node cache; loop form 5 with
+    grab 2 and longest-first order."""
+    import torch
+
+    from mirror_maze import Renderer, default_uniform, make_ext
+
+    s = _scene(32)
+    r = Renderer(0)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload_scene(s)
+    u = default_uniform(1920, 1080, 0)
+    for (y0, h, stride, F, f0) in [(0, 1080, 1, 3, 5), (3, 135, 8, 5, 0)]:
+        many, sm = r.trace_tile_frames(u, make_ext(8, 8, 8, frame=f0), F, 0, y0, 1920, h, y_stride=stride,
+                                       stats=True)
+        rays = visits = paths = 0
+        for f in range(F):
+            one, so = r.trace_tile(u, make_ext(8, 8, 8, frame=f0 + f), 0, y0, 1920, h, y_stride=stride, stats=True)
+            assert torch.equal(one.view(torch.int32), many[f].view(torch.int32)), (y0, f)
+            rays += so.rays; visits += so.node_visits; paths += so.paths
+        assert (sm.rays, sm.node_visits, sm.paths) == (rays, visits, paths)
+    r.close()
+
+
+def test_multi_frame_launch_errors(gpu):
+    from mirror_maze import MM_EXT_ACCUMULATE, MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.upload_scene(_scene(10))
+    u = default_uniform(64, 64, 0)
+    with pytest.raises(MMError):  # frames of one launch cannot accumulate
+        r.trace_tile_frames(u, make_ext(8, 3, 15, flags=MM_EXT_ACCUMULATE), 2, 0, 0, 64, 64)
+    with pytest.raises(MMError):  # 3 spp: no fused resolve
+        r.trace_tile_frames(u, make_ext(3, 3, 15), 2, 0, 0, 64, 64)
+    with pytest.raises(MMError):
+        r.trace_tile_frames(u, make_ext(8, 3, 15), 0, 0, 0, 64, 64)
+    one, _ = r.trace_tile_frames(u, make_ext(8, 3, 15, frame=4), 1, 0, 0, 64, 64)
+    ref, _ = r.trace_tile(u, make_ext(8, 3, 15, frame=4), 0, 0, 64, 64)
+    assert np.array_equal(_bits(one[0].cpu().numpy()), _bits(ref.cpu().numpy()))
+    r.close()
+
+
 def test_c4_eight_way_row_split_invariance(ren, gpu):
     """C4 (32x32 maze, 3840x2160, 16 spp, 8/15 bounces) — the multi-GPU
     config: the whole frame equals the frame assembled from the 8 interleaved
@@ -371,7 +417,7 @@ def test_large_scene_top_of_tree_cache(gpu, opts):
 
 def test_bench_prints_one_json_line(gpu):
     """bench.py's driver contract: exactly one JSON line on stdout with the
-    metric, the roofline and the issue-mode calibration (short C2 run)."""
+    metric, the roofline and the issue mode (short C2 run)."""
     import json
     import subprocess
     import sys
@@ -387,3 +433,5 @@ def test_bench_prints_one_json_line(gpu):
     assert d["unit"] == "Mrays/s" and d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
     assert d["config"]["frame_contexts"] in (1, 2)
+    assert d["config"]["frames_per_launch"] == 2  # default batching: the 2 timed frames in one launch
+    assert d["roofline"]["launches"] == 1
