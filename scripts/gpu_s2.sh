@@ -11,5 +11,5 @@ echo "== ab"; timeout -k 10 600 python scripts/ab_bench.py --frames 5 ${AB:-wp-l
 [ -z "$AB2" ] || { timeout -k 10 600 python scripts/ab_bench.py --frames 3 --config c5s $AB2 > $OUT/ab2.log 2>&1 || { tail -20 $OUT/ab2.log; exit 1; }; grep -v amdgpu.ids $OUT/ab2.log; }
 echo "== bench"; timeout -k 10 600 python bench.py --steps 10 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-echo "== rocprof"; cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/$OUT/prof -o prof -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --contexts 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/$OUT/prof.log; exit 1; }
+echo "== rocprof"; cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/$OUT/prof -o prof -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 0 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/$OUT/prof.log; exit 1; }
 cd $GRAFT_REPO_ROOT; grep -h "" $OUT/prof/prof_kernel_stats.csv | cut -c1-200; echo done
