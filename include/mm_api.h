@@ -186,6 +186,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   tile (LPT order: the cheap chunks run in the launch tail; two small sort
                                   kernels follow each launch), 0 pixel order (default: chunk durations
                                   vary too little for LPT to shorten the tail, profiles/r01_ab_chunk_order.txt) */
+#define MM_OPT_RESERVE_CUS 19 /* wave-persistent kernel: launch that many CUs' worth of resident blocks
+                                  fewer (0..128), so kernels of other streams -- a collective moving the
+                                  previous frames -- find free CUs while it runs; 0 default */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

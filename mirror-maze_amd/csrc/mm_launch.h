@@ -43,6 +43,8 @@ struct TileJob {
     // resolve): the queue holds n_frames frames' chunks back to back; frame f
     // uses RNG frame e.frame + f and writes out + f * w * h.
     uint32_t n_frames = 1;
+    // CUs' worth of blocks the wave-persistent grid leaves free (MM_OPT_RESERVE_CUS)
+    uint32_t reserve_cus = 0;
 };
 
 struct MegaOpts {

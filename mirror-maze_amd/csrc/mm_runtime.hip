@@ -93,6 +93,7 @@ struct mm_ctx {
     uint32_t opt_fair = 0;       // MM_OPT_FAIR: issue priority for waves behind the mean chunk count
     uint32_t opt_grab = 1;       // chunks per work-counter atomic
     bool opt_blocksync = false;  // block-synchronous bounces with ray compaction (trace_block.hip)
+    uint32_t opt_reserve_cus = 0;  // MM_OPT_RESERVE_CUS
     uint32_t opt_chunk_order = 0;  // MM_OPT_CHUNK_ORDER: 0 pixel order, 1 longest first (previous launch)
     // longest-first chunk order (chunk_order.hip): durations of the last launch
     // of the tile `order_key` describes, the permutation sorted from them
@@ -365,6 +366,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
         case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
         case MM_OPT_BLOCKSYNC: c->opt_blocksync = value != 0; return MM_OK;
+        case MM_OPT_RESERVE_CUS:
+            if (value < 0 || value > 128) return fail(c, MM_ERR_INVALID, "reserved CUs must be 0..128");
+            c->opt_reserve_cus = (uint32_t)value;
+            return MM_OK;
         case MM_OPT_CHUNK_ORDER:
             if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "chunk order must be 0 or 1");
             c->opt_chunk_order = (uint32_t)value;
@@ -682,6 +687,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.wave_ts_cap = c->wave_ts_cap;
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
+        job.reserve_cus = c->opt_reserve_cus;
         uint32_t sort_chunks = 0;  // > 0: queue the longest-first sort of this launch's chunk durations
         if (c->opt_tail_gate) HIPC(c, launch_tail_gate(c->stream));
         if ((rc = prof_mark(c))) return rc;

@@ -421,7 +421,9 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t n_paths = job.w * job.h * job.e.spp;
-    uint32_t grid = (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus);
+    // MM_OPT_RESERVE_CUS: leave that many CUs' worth of resident blocks free for other work (collectives)
+    const int cus_used = std::max(1, cus - (int)job.reserve_cus);
+    uint32_t grid = (uint32_t)std::max(1, per_cu) * (uint32_t)cus_used;
     grid = std::max(1u, std::min(grid, (n_paths + block - 1) / block));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, s, sc, job, samples, stats, err, work, stack_slots);
     return hipGetLastError();
