@@ -183,14 +183,17 @@ def main():
     frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     # one RCCL gather per frame, issued async on the frame's stream into
     # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
-    gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf, slots=max(2, len(rens)),
+    fb_max = 1 if args.accumulate else (args.batch if args.batch > 0 else 8)
+    # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,
+    # so the next launch never waits on this batch's own gathers
+    gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf,
+                              slots=max(2, len(rens), 2 * fb_max if fb_max > 1 else 0),
                               assembly_stream=torch.cuda.Stream(dev))
                 if distributed else None)
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in rens]
     last = [0]
     active = [len(rens)]  # contexts the frames alternate over
     batch = [1]           # frames per launch (mm_trace_tile_frames), single context
-    fb_max = 1 if args.accumulate else (args.batch if args.batch > 0 else 8)
     batch_buf = torch.zeros((fb_max, my_rows, W, 4), dtype=torch.float32, device=dev) if fb_max > 1 else None
     progress_t = [time.perf_counter()]
 
