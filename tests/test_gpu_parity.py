@@ -273,12 +273,12 @@ def test_chunk_order_bit_identical(gpu):
     lpt.close()
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 2}, {7: 5, 15: 2, 17: 1}])
+@pytest.mark.parametrize("opts", [{}, {9: 2}, {7: 5, 15: 2, 17: 1}, {19: 8}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole
     frames and a row-split tile; the split node cache; loop form 5 with
-    grab 2 and longest-first order."""
+    grab 2 and longest-first order; a grid 8 CUs short (MM_OPT_RESERVE_CUS)."""
     import torch
 
     from mirror_maze import Renderer, default_uniform, make_ext
