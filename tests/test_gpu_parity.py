@@ -435,3 +435,25 @@ def test_bench_prints_one_json_line(gpu):
     assert d["config"]["frame_contexts"] in (1, 2)
     assert d["config"]["frames_per_launch"] == 2  # default batching: the 2 timed frames in one launch
     assert d["roofline"]["launches"] == 1
+
+
+def test_bench_issue_mode_calibration(gpu):
+    """bench.py --batch 0 times one context, two contexts and batches of 8
+    after warmup and reports all three; --batch 1 --contexts 2 alternates
+    single-frame launches over two contexts."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    for extra, check in ((["--batch", "0"], lambda d: set(d["config"]["frame_contexts_calibration_ms"]) ==
+                          {"1", "2", "batch8"}),
+                         (["--batch", "1", "--contexts", "2"], lambda d: d["config"]["frame_contexts"] == 2 and
+                          d["config"]["frames_per_launch"] == 1 and d["roofline"]["launches"] == 3)):
+        r = subprocess.run([sys.executable, str(repo / "bench.py"), "--config", "c1", "--steps", "3", "--warmup", "1",
+                            "--no-cpu-baseline"] + extra, capture_output=True, text=True, timeout=240, cwd=repo)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+        assert len(lines) == 1, r.stdout
+        assert check(json.loads(lines[0])), lines[0]
