@@ -361,8 +361,9 @@ def main():
         achieved = alg_bytes / k_avg_s / 1e9
         traffic = None
         tf = REPO / "profiles" / f"traffic_{args.config}_{args.pipeline}.json"
-        if tf.exists() and not args.emulate_ranks:  # measured on one-frame, whole-frame launches: x frames/launch
-            t1 = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+        if tf.exists() and not args.emulate_ranks:  # measured on whole-frame launches: per frame x frames/launch
+            rec = json.loads(tf.read_text())
+            t1 = rec.get("hbm_bytes_per_frame", rec.get("hbm_bytes_per_launch"))
             traffic = None if t1 is None or world > 1 else round(t1 * args.steps / max(k_launches, 1))
         valu_ops = (25 * 2 * (visits / max(k_launches, 1)) + 71 * (rtests / max(k_launches, 1)))
         line = {

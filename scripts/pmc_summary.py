@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc passes (scripts/pmc.sh output) for one kernel.
 
-    python scripts/pmc_summary.py gpurun_out/<tag> [kernel-substring [traffic.json]] > profiles/<name>.txt
+    python scripts/pmc_summary.py gpurun_out/<tag> [kernel-substring [traffic.json [frames-per-launch]]] > profiles/<name>.txt
 Per-dispatch means of every counter, plus derived metrics:
   lane utilisation = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
   VALU issue share = SQ_INSTS_VALU / (SIMDs * cycles / 2)   (wave64 VALU = 2 cycles on SIMD32)
@@ -40,8 +40,11 @@ if "WRITE_SIZE" in m:
 if len(sys.argv) > 3 and "FETCH_SIZE" in m and "WRITE_SIZE" in m:
     # bench.py reads this as roofline.traffic (HBM bytes per launch of the dominant kernel)
     import json
+    frames = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0  # frames per profiled launch
+    per_launch = 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
     rec = {"kernel_pattern": pat, "source": root.name,
            "fetch_bytes_corrected": 2 * m["FETCH_SIZE"] * 1024, "write_bytes": m["WRITE_SIZE"] * 1024,
-           "hbm_bytes_per_launch": 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024,
+           "hbm_bytes_per_launch": per_launch, "frames_per_launch": frames,
+           "hbm_bytes_per_frame": per_launch / frames,
            "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, per-dispatch mean"}
     Path(sys.argv[3]).write_text(json.dumps(rec, indent=1) + "\n")
