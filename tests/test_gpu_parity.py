@@ -289,12 +289,14 @@ def test_multi_frame_launch_bit_identical(gpu, opts):
         r.set_option(k, v)
     r.upload_scene(s)
     u = default_uniform(1920, 1080, 0)
-    for (y0, h, stride, F, f0) in [(0, 1080, 1, 3, 5), (3, 135, 8, 5, 0)]:
-        many, sm = r.trace_tile_frames(u, make_ext(8, 8, 8, frame=f0), F, 0, y0, 1920, h, y_stride=stride,
+    # whole frames, a row-split tile, and a ragged 37x13 tile (each frame's last chunk partial)
+    for (x0, y0, w, h, stride, F, f0) in [(0, 0, 1920, 1080, 1, 3, 5), (0, 3, 1920, 135, 8, 5, 0),
+                                          (101, 200, 37, 13, 3, 4, 9)]:
+        many, sm = r.trace_tile_frames(u, make_ext(8, 8, 8, frame=f0), F, x0, y0, w, h, y_stride=stride,
                                        stats=True)
         rays = visits = paths = 0
         for f in range(F):
-            one, so = r.trace_tile(u, make_ext(8, 8, 8, frame=f0 + f), 0, y0, 1920, h, y_stride=stride, stats=True)
+            one, so = r.trace_tile(u, make_ext(8, 8, 8, frame=f0 + f), x0, y0, w, h, y_stride=stride, stats=True)
             assert torch.equal(one.view(torch.int32), many[f].view(torch.int32)), (y0, f)
             rays += so.rays; visits += so.node_visits; paths += so.paths
         assert (sm.rays, sm.node_visits, sm.paths) == (rays, visits, paths)
