@@ -161,7 +161,8 @@ def main():
     # renderer contexts on their own streams so frame k+1's blocks fill the
     # CUs frame k's tail leaves idle (two frames sharing the GPU run ~7 %
     # slower, profiles/r01_overlap_probe.txt; --contexts 0 times both).
-    n_ctx = 1 if args.accumulate or args.batch > 1 else (args.contexts if args.contexts > 0 else 2)
+    n_ctx = (1 if args.accumulate or (args.batch > 1 and args.pipeline != "wave" and 64 % spp == 0)
+             else (args.contexts if args.contexts > 0 else 2))
     rens = []
     for _ in range(n_ctx):
         r = Renderer(local)
@@ -183,7 +184,9 @@ def main():
     frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
     # one RCCL gather per frame, issued async on the frame's stream into
     # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
-    fb_max = 1 if args.accumulate else (args.batch if args.batch > 0 else 8)
+    # multi-frame launches need the wave-persistent kernel's fused resolve (64 % spp == 0)
+    batchable = not args.accumulate and args.pipeline != "wave" and 64 % spp == 0
+    fb_max = (args.batch if args.batch > 0 else 8) if batchable else 1
     # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,
     # so the next launch never waits on this batch's own gathers
     gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf,
@@ -271,7 +274,7 @@ def main():
         if not gatherer:
             frame_buf.copy_(tiles1[last[0]])
 
-    if args.batch > 1 and not args.accumulate:  # warm up the issue mode that is timed
+    if fb_max > 1 and args.batch > 1:  # warm up the issue mode that is timed
         batch[0] = fb_max
         run_frames(0, 10_000, args.warmup)
     else:
@@ -279,11 +282,12 @@ def main():
             step(i, 10_000 + i)
     drain()
     calib = None
-    if args.batch > 1 and not args.accumulate:
+    if fb_max > 1 and args.batch > 1:
         active[0], batch[0] = 1, fb_max
     elif (args.batch == 0 or args.contexts == 0) and not args.accumulate:
         # issue modes: one context, two alternating contexts, one context with batches of frames
-        modes = [("1", 1, 1), ("2", 2, 1)] + ([(f"batch{fb_max}", 1, fb_max)] if args.batch == 0 else [])
+        modes = [("1", 1, 1), ("2", 2, 1)] + ([(f"batch{fb_max}", 1, fb_max)] if args.batch == 0 and fb_max > 1
+                                             else [])
         calib = {}
         for rep in range(2):
             for name, m, fb in modes:
