@@ -74,6 +74,19 @@ def parse():
     return p.parse_args()
 
 
+def launch_sizes(count: int, per_launch: int) -> list:
+    """Frames per launch for `count` consecutive frames, at most `per_launch`
+    each: ceil(count / per_launch) launches of sizes as equal as possible."""
+    if count <= 0:
+        return []
+    n = -(-count // per_launch)
+    sizes, left = [], count
+    for j in range(n):
+        sizes.append(left // (n - j))
+        left -= sizes[-1]
+    return sizes
+
+
 def cpu_baseline(scene, u, ext, W, H, budget_s):
     """Oracle (CPU restatement, oracle/mm_oracle.c -O2 scalar) on a bounded row
     sample of the same workload, one thread per core, GIL released in C."""
@@ -241,11 +254,9 @@ def main():
 
     def run_frames(k0, frame0, count):
         """count frames starting at frame0 in the current issue mode"""
-        if batch[0] > 1:  # ceil(count / batch) launches of as equal sizes as possible
-            n_launch = -(-count // batch[0])
-            i = 0
-            for j in range(n_launch):
-                n = (count - i) // (n_launch - j)
+        if batch[0] > 1:
+            i = n = 0
+            for n in launch_sizes(count, batch[0]):
                 step_batch(k0 + i, frame0 + i, n)
                 i += n
             if not gatherer and count > 0:  # the last frame, for frame_buf
