@@ -189,6 +189,11 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_RESERVE_CUS 19 /* wave-persistent kernel: launch that many CUs' worth of resident blocks
                                   fewer (0..128), so kernels of other streams -- a collective moving the
                                   previous frames -- find free CUs while it runs; 0 default */
+#define MM_OPT_DICT_NODES 20  /* wave-persistent kernel, loop form 5/7: BVH nodes dictionary-coded (8-bit
+                                  indices into the scene's <= 256 distinct bound values, 12 B per node) so
+                                  the whole tree sits in LDS: 1 where the split cache would be used (default:
+                                  C5 scene 29.5 -> 26.1 ms), 2 always (tests; on trees that fit plain it
+                                  only adds decoding: C3 9.6 -> 12.1 ms), 0 off */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

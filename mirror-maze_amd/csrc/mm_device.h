@@ -47,6 +47,11 @@ struct DevScene {
     const float4* nodes_exact;  // 2 * n_nodes, production layout, exact bounds
     const float4* slot_box;     // 2 per slot: (mn.x, mx.x, mn.y, mx.y), (mn.z, mx.z, 0, 0) of its leaf
     float cons_bound;           // |ray origin component| must be <= this for the search (else exact)
+    // Dictionary-coded nodes (LDS mode 10, MM_OPT_DICT_NODES): the distinct bound
+    // values (<= 256) and 3 words per production node: 8-bit indices of
+    // (mn.x, mx.x, mn.y, mx.y), of (mn.z, mx.z), and the packed child word
+    const float* dict_tab;      // 256 floats
+    const uint32_t* dict_words; // 3 * n_nodes
 };
 
 // ---- IEEE helpers (the AIR intrinsics with their IEEE meaning) -------------

@@ -43,6 +43,9 @@ struct mm_ctx {
     uint2* d_recs = nullptr;    // compact leaf-ordered rect records
     size_t n_fast_recs = 0;
     bool lean_ok = false;       // no SLOW rect records (loop forms 7, 9)
+    float* d_dict_tab = nullptr;       // dictionary-coded nodes (mode 10): 256 values
+    uint32_t* d_dict_words = nullptr;  // 3 words per production node
+    bool dict_ok = false;
     float4* d_nodes_cons = nullptr;  // production layout, boxes expanded by the search margin (form 9)
     float4* d_slot_box = nullptr;    // per BVH slot: its leaf's exact box (form 9 verification)
     float cons_bound = 0.0f;         // |coordinate| bound of the scene (form 9 ray guard)
@@ -94,6 +97,7 @@ struct mm_ctx {
     uint32_t opt_grab = 1;       // chunks per work-counter atomic
     bool opt_blocksync = false;  // block-synchronous bounces with ray compaction (trace_block.hip)
     uint32_t opt_reserve_cus = 0;  // MM_OPT_RESERVE_CUS
+    uint32_t opt_dict = 1;         // MM_OPT_DICT_NODES: 0 off, 1 instead of the split cache (default), 2 always
     uint32_t opt_chunk_order = 0;  // MM_OPT_CHUNK_ORDER: 0 pixel order, 1 longest first (previous launch)
     // longest-first chunk order (chunk_order.hip): durations of the last launch
     // of the tile `order_key` describes, the permutation sorted from them
@@ -145,6 +149,8 @@ DevScene dev_scene(const mm_ctx* c) {
     s.nodes_exact = c->d_nodes;
     s.slot_box = c->d_slot_box;
     s.cons_bound = c->cons_bound;
+    s.dict_tab = c->d_dict_tab;
+    s.dict_words = c->d_dict_words;
     s.shade = c->d_shade;
     s.idx = c->d_idx;
     s.n_nodes = c->n_nodes;
@@ -157,6 +163,8 @@ void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
     (void)hipFree(c->d_nodes_cons); (void)hipFree(c->d_slot_box);
     c->d_nodes_cons = nullptr; c->d_slot_box = nullptr;
+    (void)hipFree(c->d_dict_tab); (void)hipFree(c->d_dict_words);
+    c->d_dict_tab = nullptr; c->d_dict_words = nullptr; c->dict_ok = false;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
     c->has_scene = false;
 }
@@ -366,6 +374,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
         case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
         case MM_OPT_BLOCKSYNC: c->opt_blocksync = value != 0; return MM_OK;
+        case MM_OPT_DICT_NODES:
+            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
+            c->opt_dict = (uint32_t)value;
+            return MM_OK;
         case MM_OPT_RESERVE_CUS:
             if (value < 0 || value > 128) return fail(c, MM_ERR_INVALID, "reserved CUs must be 0..128");
             c->opt_reserve_cus = (uint32_t)value;
@@ -452,6 +464,38 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
             packed[2 * i] = make_float4(nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1]);
             packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
         }
+    // Dictionary-coded nodes (mode 10): the distinct bound values of the
+    // production array, 8-bit indices when there are at most 256
+    std::vector<float> dict;
+    for (const float4& f : packed) {
+        dict.push_back(f.x);
+        dict.push_back(f.y);
+    }
+    for (size_t i = 0; i < packed.size(); i += 2) {
+        dict.push_back(packed[i].z);
+        dict.push_back(packed[i].w);
+    }
+    auto fbits = [](float x) { uint32_t b; std::memcpy(&b, &x, 4); return b; };
+    std::sort(dict.begin(), dict.end(), [&](float a, float b) { return fbits(a) < fbits(b); });
+    dict.erase(std::unique(dict.begin(), dict.end(), [&](float a, float b) { return fbits(a) == fbits(b); }),
+               dict.end());
+    const bool dict_ok = dict.size() <= 256;
+    std::vector<uint32_t> dict_words;
+    if (dict_ok) {
+        auto code = [&](float x) {
+            const uint32_t b = fbits(x);
+            return (uint32_t)(std::lower_bound(dict.begin(), dict.end(), x,
+                                               [&](float a, float) { return fbits(a) < b; }) - dict.begin());
+        };
+        dict_words.resize(3 * (size_t)n_prod);
+        for (uint32_t i = 0; i < n_prod; ++i) {
+            const float4 a = packed[2 * (size_t)i], b = packed[2 * (size_t)i + 1];
+            dict_words[3 * (size_t)i] = code(a.x) | code(a.y) << 8 | code(a.z) << 16 | code(a.w) << 24;
+            dict_words[3 * (size_t)i + 1] = code(b.x) | code(b.y) << 8;
+            dict_words[3 * (size_t)i + 2] = fbits(b.z);
+        }
+        dict.resize(256, 0.0f);
+    }
     // Verified conservative search (form 9): boxes expanded outward by
     // E = C * 2^-14, C = the scene's largest |coordinate| (>= 64x the rounding
     // bound of mm_trace.h: traverse_cons), and each slot's exact leaf box.
@@ -512,6 +556,13 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     HIPC(c, hipMemcpyAsync(c->d_slot_box, slot_box.data(), slot_box.size() * sizeof(float4), hipMemcpyHostToDevice,
                            c->stream));
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    if (dict_ok) {
+        HIPC(c, hipMalloc((void**)&c->d_dict_tab, 256 * sizeof(float)));
+        HIPC(c, hipMalloc((void**)&c->d_dict_words, dict_words.size() * sizeof(uint32_t)));
+        HIPC(c, hipMemcpyAsync(c->d_dict_tab, dict.data(), 256 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->d_dict_words, dict_words.data(), dict_words.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, c->stream));
+    }
     HIPC(c, hipMemcpyAsync(c->d_idx, idx, n_rects * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));  // host arrays may be freed on return
@@ -523,6 +574,7 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     c->fast_ok = fast;
     c->cons_bound = cbound;
     c->lean_ok = n_slow == 0;
+    c->dict_ok = dict_ok;
     c->has_scene = true;
     return MM_OK;
 }
@@ -761,11 +813,16 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                 sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
                 mode = ((ww == 0 || ww == 5 || ww == 7 || ww == 9) && c->opt_glob_rects != 0) ? 6 : 4;
             }
+            // dictionary-coded nodes, all in LDS (mode 10): instead of the split cache (1) or always (2)
+            const size_t lds_dict = 256 * sizeof(float) + 12 * (size_t)c->n_nodes;
+            if (c->opt_dict && c->dict_ok && (ww == 5 || ww == 7) && block == 1024 && c->opt_min_waves == 8 &&
+                lds_dict <= lds_budget && (c->opt_dict == 2 || mode == 6 || mode == 4))
+                mode = 10;
             // the lean and verified-search forms need compact records for every leaf (modes 3,
             // 6, 7) and a lean scene (no SLOW records); auto prefers the lean form
             // (C3 10.40 -> 9.56 ms, profiles/r01_ab_lean.txt)
             const bool lean_fits = c->lean_ok && block == 1024 && c->opt_min_waves == 8 &&
-                                   (mode == 3 || mode == 6 || mode == 7);
+                                   (mode == 3 || mode == 6 || mode == 7 || mode == 10);
             // (auto: not with the split node cache, where it measured 30.6 vs 29.4 ms on the C5 scene)
             if (c->opt_ww < 0 && ww == 5 && lean_fits && mode != 6) ww = 7;
             if ((ww == 7 || ww == 9) && !lean_fits) ww = 5;

@@ -221,6 +221,26 @@ __device__ __forceinline__ void node_pair(const SplitNodes& n, uint32_t lf, floa
     else node_pair(n.glob, lf, la, lb, ra, rb);
 }
 
+// Dictionary-coded nodes in LDS (mode 10): 12 B per node, so the N=64 tree
+// (5534 nodes, 66 KB + a 1 KB value table) fits the LDS budget.  Decoding
+// returns the production layout's values exactly (the table holds the
+// original floats).  Left children sit at even production indices, so a pair
+// (24 B at 12 * lf) is 8-B aligned.
+struct DictNodes {
+    const uint32_t* w;   // 3 words per node
+    const float* tab;    // 256 bound values
+};
+__device__ __forceinline__ void node_pair(const DictNodes& n, uint32_t lf, float4& la, float4& lb, float4& ra,
+                                          float4& rb) {
+    const uint2* p = reinterpret_cast<const uint2*>(n.w + 3 * lf);
+    const uint2 q0 = p[0], q1 = p[1], q2 = p[2];
+    // left child: q0.x (4 indices), q0.y (2 indices), q1.x packed; right: q1.y, q2.x, q2.y
+    la = make_float4(n.tab[q0.x & 255u], n.tab[(q0.x >> 8) & 255u], n.tab[(q0.x >> 16) & 255u], n.tab[q0.x >> 24]);
+    lb = make_float4(n.tab[q0.y & 255u], n.tab[(q0.y >> 8) & 255u], __uint_as_float(q1.x), 0.0f);
+    ra = make_float4(n.tab[q1.y & 255u], n.tab[(q1.y >> 8) & 255u], n.tab[(q1.y >> 16) & 255u], n.tab[q1.y >> 24]);
+    rb = make_float4(n.tab[q2.x & 255u], n.tab[(q2.x >> 8) & 255u], __uint_as_float(q2.y), 0.0f);
+}
+
 __device__ __forceinline__ float sel3(uint32_t a, F3 v) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
 
 // ray_rect_intersect on a compact record (FAST kind) for a fast-guarded ray;

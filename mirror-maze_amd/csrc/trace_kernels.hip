@@ -311,7 +311,8 @@ template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, Scr
 // 5 nodes in LDS + each path's T and L parked in LDS while it traverses,
 // 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same,
 // 8 = 2 + the same (nodes and u16 stack in LDS, rect records via L1/L2),
-// 9 = 3 with u16 traversal-stack entries in scratch.
+// 9 = 3 with u16 traversal-stack entries in scratch, 10 dictionary-coded nodes
+// in LDS (DictNodes) + compact rect records read through L1/L2.
 // Diagnostics: time at which the block's LDS staging completed (wave timeline).
 #define MM_TS_STAGED()                                                                                      \
     do {                                                                                                     \
@@ -339,6 +340,17 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
             chunks = wp_dispatch<kStats, kWW>(sc, view(nodes, sc.recs), st, job, samples, stats, err, work);
         else
             chunks = wp_dispatch<kStats, kWW>(sc, view(nodes), st, job, samples, stats, err, work);
+    } else if constexpr (kLds == 10) {  // dictionary-coded nodes in LDS, compact rect records via L1/L2
+        extern __shared__ float4 lds_dict[];
+        float* tab = reinterpret_cast<float*>(lds_dict);
+        uint32_t* words = reinterpret_cast<uint32_t*>(tab + 256);
+        for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = sc.dict_tab[i];
+        for (uint32_t i = threadIdx.x; i < 3 * sc.n_nodes; i += blockDim.x) words[i] = sc.dict_words[i];
+        __syncthreads();
+        MM_TS_STAGED();
+        WpStack<kWW> st;
+        chunks = wp_dispatch<kStats, kWW>(sc, view(DictNodes{words, tab}, sc.recs), st, job, samples, stats, err,
+                                          work);
     } else if constexpr (kLds == 7) {
         extern __shared__ float4 lds_nodes7[];
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes7[i] = sc.nodes[i];
@@ -408,7 +420,8 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        uint32_t stack_slots, hipStream_t s) {
     const uint32_t block = kBlock;
-    const size_t lds = (kLds == 4 || kLds == 6) ? (size_t)sc.n_lds_f4 * sizeof(float4)
+    const size_t lds = kLds == 10 ? 256 * sizeof(float) + 3 * (size_t)sc.n_nodes * sizeof(uint32_t)
+                     : (kLds == 4 || kLds == 6) ? (size_t)sc.n_lds_f4 * sizeof(float4)
                                  : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
                                        (kLds == 5 ? 6 * (size_t)block * sizeof(float) : 0) +
                                        (kLds == 2 || kLds == 8 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
@@ -450,10 +463,13 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
     MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
     if (block == 1024 && min_waves == 8 && loop_form == 5) {
         MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP2(8, 1024, 8, 5) MM_WP2(9, 1024, 8, 5)
+        MM_WP2(10, 1024, 8, 5)
         MM_WP3(1024, 8, 5)
     }
     if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
-    if (block == 1024 && min_waves == 8 && loop_form == 7) { MM_WP2(3, 1024, 8, 7) MM_WP2(6, 1024, 8, 7) MM_WP2(7, 1024, 8, 7) }
+    if (block == 1024 && min_waves == 8 && loop_form == 7) {
+        MM_WP2(3, 1024, 8, 7) MM_WP2(6, 1024, 8, 7) MM_WP2(7, 1024, 8, 7) MM_WP2(10, 1024, 8, 7)
+    }
     if (block == 1024 && min_waves == 8 && loop_form == 9) { MM_WP2(3, 1024, 8, 9) MM_WP2(6, 1024, 8, 9) MM_WP2(7, 1024, 8, 9) }
     // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS
     if (block == 768 && min_waves == 6 && loop_form == 5) { MM_WP2(3, 768, 6, 5) MM_WP2(6, 768, 6, 5) }

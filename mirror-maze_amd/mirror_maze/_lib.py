@@ -36,7 +36,7 @@ MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_THRESHOLD, MM_OPT_MIN_WAVES, MM_OPT_LDS_STACK = 1, 2, 3, 4, 5, 6
 MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS, MM_OPT_LDS_SPLIT, MM_OPT_COLD_LDS, MM_OPT_GLOBAL_RECTS = 7, 8, 9, 10, 11
 MM_OPT_FUSE_RESOLVE, MM_OPT_TAIL_GATE, MM_OPT_FAIR, MM_OPT_GRAB, MM_OPT_BLOCKSYNC = 12, 13, 14, 15, 16
-MM_OPT_CHUNK_ORDER, MM_OPT_RESERVE_CUS = 17, 19
+MM_OPT_CHUNK_ORDER, MM_OPT_RESERVE_CUS, MM_OPT_DICT_NODES = 17, 19, 20
 MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1

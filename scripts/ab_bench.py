@@ -70,6 +70,9 @@ VARIANTS["brli-ldsrec"] = dict(pipe=1, persist=2, lds=1, block=1024, mw=8, ls=0,
 VARIANTS["blocksync"] = dict(pipe=1, bsync=1)
 VARIANTS["lean7"] = dict(pipe=1, ww=7)
 VARIANTS["order1"] = dict(pipe=1, order=1)
+VARIANTS["dict"] = dict(pipe=1, dict=1)
+VARIANTS["dict-li"] = dict(pipe=1, dict=1, ww=5)
+VARIANTS["dict2"] = dict(pipe=1, dict=2)
 VARIANTS["cons9"] = dict(pipe=1, ww=9)
 VARIANTS["li-ldsstack-grec"] = dict(pipe=1, ls=2)
 VARIANTS["li-ldsstack"] = dict(pipe=1, ls=1, lr=0)
@@ -126,6 +129,8 @@ def main():
             r.set_option(16, v["bsync"])
         if "grab" in v:
             r.set_option(15, v["grab"])
+        if "dict" in v:
+            r.set_option(20, v["dict"])
         if "order" in v:
             r.set_option(17, v["order"])
         if "fair" in v:

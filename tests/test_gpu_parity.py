@@ -140,6 +140,8 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     "blocksync": (1, {3: 2, 16: 1}),
     "leanli": (1, {3: 2, 7: 7}),
     "leanli-order": (1, {3: 2, 7: 7, 17: 1}),
+    "leanli-dict": (1, {3: 2, 7: 7, 20: 2}),
+    "leafinterior-dict": (1, {3: 2, 7: 5, 20: 2}),
     "leafinterior-order-grab2": (1, {3: 2, 7: 5, 17: 1, 15: 2}),
     "cons": (1, {3: 2, 7: 9}),
     "cons-split2kb": (1, {3: 2, 7: 9, 9: 2}),
@@ -193,7 +195,7 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
                                   "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
                                   "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
                                   "leafinterior-grab3-fair", "blocksync", "leanli", "cons", "leanli-order",
-                                  "leafinterior-order-grab2"])
+                                  "leafinterior-order-grab2", "leanli-dict", "leafinterior-dict"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -387,9 +389,10 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}, {7: 7}, {7: 9}],
+@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}, {7: 7}, {7: 9},
+                                  {20: 1}, {20: 1, 7: 5}],
                          ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects",
-                              "leafinterior", "ifif", "leanli", "cons"])
+                              "leafinterior", "ifif", "leanli", "cons", "dict", "dict-leafinterior"])
 def test_large_scene_top_of_tree_cache(gpu, opts):
     """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
     default kernel caches the top of the breadth-first node array in LDS and
