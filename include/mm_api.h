@@ -110,7 +110,10 @@ int  mm_quantize_rgba8(mm_ctx* ctx, const float* rgba_dev, uint8_t* rgba8_dev, u
  * out_dev: caller DEVICE pointer to w*h float4 (row-major over (j,i));
  * alpha = 1 (or, with MM_EXT_ACCUMULATE, += the frame value, alpha += 1).
  * stats: optional host pointer; filled after an implicit sync when
- * MM_EXT_COUNT_STATS is set. */
+ * MM_EXT_COUNT_STATS is set.  rays and paths are exact; node_visits and
+ * rect_tests count the work of the query method that ran (BVH: interior
+ * nodes expanded and rect tests; grid search: cells visited and rect tests,
+ * plus the BVH walk's counts for the queries that fell back to it). */
 int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
                    uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
                    uint32_t y_stride, float* out_dev, mm_stats* stats);
@@ -136,65 +139,57 @@ int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
                                   (IEEE division everywhere); A/B baseline  */
 int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 
-/* Tuning knobs (results never change; only speed does). */
-#define MM_OPT_LDS_NODES   1   /* 1: stage the BVH in LDS when it fits (default), 0: read via L1/L2 */
-#define MM_OPT_BLOCK       2   /* threads per workgroup for the megakernel (64..1024, multiple of 64) */
-#define MM_OPT_PERSIST     3   /* 0: one thread per path, 1: persistent lane-refill megakernel,
-                                  2: wave-persistent megakernel, 64-path chunks (default) */
-#define MM_OPT_THRESHOLD   4   /* persistent kernel: traverse while > N lanes traverse (0..63) */
-#define MM_OPT_MIN_WAVES   5   /* wave-persistent kernel register budget: 1, 6 or 8 (default) waves/SIMD */
-#define MM_OPT_TRAVERSAL   7   /* wave-persistent kernel loop form: 0 if-if, 1 while-while,
-                                  2 lean if-if (one pop site, no overflow test),
-                                  3 if-if with the stack top in a register,
-                                  4 if-if, lanes refilled with new paths at every bounce,
-                                  5 leaf tests and the next interior step in one iteration (1024/8 only),
-                                  6 bounce refill with form 5's traversal,
-                                  7 form 5 with branch-free compact leaf tests and no push overflow test
-                                    (scenes without SLOW rect records),
-                                  9 verified conservative search (approximate slab quotients on expanded
-                                    boxes, exact rect tests, exact check of the winner's leaf box;
-                                    bit-identical results, slower on the maze: experimental),
-                                  -1 auto: 7 when the scene allows, else 5 at 1024 threads / 8 waves,
-                                    else 0 (default)
-                                  8 / 16 / 32: leaf batching (leaf tests once >= N lanes wait) */
-#define MM_OPT_LDS_RECTS   8   /* wave-persistent kernel: 1 compact rect records in LDS when they fit (default) */
-#define MM_OPT_LDS_STACK   6   /* wave-persistent kernel: 1 u16 traversal stack in LDS when it fits, 2 the same
-                                  with the compact rect records through L1/L2 (loop form 5), 3 u16 entries in
-                                  scratch (loop form 5), 0 u32 entries in scratch (default) */
-#define MM_OPT_LDS_SPLIT   9   /* wave-persistent kernel, BVH larger than the LDS budget: cache the top of
-                                  the (breadth-first) node array in LDS, rest via L1/L2.
-                                  0 off, 1 auto size (default), >1: always use a cache of this many KB */
-#define MM_OPT_COLD_LDS   10   /* wave-persistent kernel: 1 park each path's T and L in LDS while its ray
-                                  traverses (frees registers; nodes in LDS, no rect records), 0 off (default) */
-#define MM_OPT_GLOBAL_RECTS 11 /* wave-persistent kernel, rect records not staged in LDS: leaf tests read the
-                                  compact records through L1/L2 -- 0 never (general test), 1 always,
-                                  2 with the split node cache only (default) */
+/* Tuning knobs (results never change; only speed does).  Every value is
+ * bit-identical to the reference; the defaults are the measured fastest
+ * (DESIGN.md §4).  Options removed after round 1 (measured slower or
+ * neutral: 4, 5, 6, 10, 11, 13-17) return MM_ERR_INVALID. */
+#define MM_OPT_LDS_NODES   1   /* 1: stage scene data (BVH or grid) in LDS where it fits (default), 0: read
+                                  everything through L1/L2 */
+#define MM_OPT_BLOCK       2   /* threads per workgroup of the one-thread-per-path kernel (64..1024, x64) */
+#define MM_OPT_PERSIST     3   /* 2: wave-persistent kernel, 64-path chunks, pixels resolved in the wave
+                                  (default), 0: one thread per path (k_trace_mega) */
+#define MM_OPT_TRAVERSAL   7   /* closest-hit query of the wave-persistent kernel:
+                                  -1 auto (default): 11 when the scene allows it, else 7 when every rect has a
+                                     compact record, else 5;
+                                  11 certified grid search (mm_grid.h): same answer as the reference's BVH walk,
+                                     which runs instead on ties / failed certificates / rays outside the grid;
+                                  0 the reference's BVH loop, one step per iteration (nodes in LDS only);
+                                  5 BVH, leaf tests and the next interior step in one iteration;
+                                  7 form 5 with branch-free compact leaf tests (scenes without SLOW records) */
+#define MM_OPT_LDS_RECTS   8   /* BVH forms: 1 compact rect records in LDS beside the nodes when both fit (default) */
+#define MM_OPT_LDS_SPLIT   9   /* BVH forms, nodes larger than the LDS budget: cache the top of the
+                                  (breadth-first) node array in LDS, rest via L1/L2.  0 off, 1 auto size where
+                                  dictionary nodes do not fit (default), >1: always a cache of this many KB
+                                  (wins over MM_OPT_DICT_NODES 1) */
 #define MM_OPT_FUSE_RESOLVE 12 /* wave-persistent kernel: 1 reduce each pixel's samples inside the wave
                                   that traced them when 64 % spp == 0 (default), 0 separate k_resolve */
-#define MM_OPT_TAIL_GATE  13  /* 1: queue a one-wave no-op ahead of every trace launch, so that when
-                                  several contexts' frames share the GPU a frame starts on the CUs the
-                                  previous frame's tail frees, not alongside it (0 default) */
-#define MM_OPT_FAIR       14  /* wave-persistent kernel: 1 raise the issue priority of waves behind the
-                                  mean chunk count (evens out per-wave progress), 0 default */
-#define MM_OPT_GRAB       15  /* wave-persistent kernel: 64-path chunks a wave claims per atomic on the
-                                  work counter, 1..16 (1 default) */
-#define MM_OPT_BLOCKSYNC  16  /* 1: block-synchronous bounces, the live rays of each 1024-path block
-                                  compacted before every closest-hit pass (experimental; nodes must
-                                  fit 47 KB of LDS beside the 32 KB exchange), 0 default */
-#define MM_OPT_CHUNK_ORDER 17 /* wave-persistent kernel, frame in one launch: 1 hand out the 64-path chunks
-                                  longest first, by their durations in the previous launch of the same
-                                  tile (LPT order: the cheap chunks run in the launch tail; two small sort
-                                  kernels follow each launch), 0 pixel order (default: chunk durations
-                                  vary too little for LPT to shorten the tail, profiles/r01_ab_chunk_order.txt) */
 #define MM_OPT_RESERVE_CUS 19 /* wave-persistent kernel: launch that many CUs' worth of resident blocks
                                   fewer (0..128), so kernels of other streams -- a collective moving the
                                   previous frames -- find free CUs while it runs; 0 default */
-#define MM_OPT_DICT_NODES 20  /* wave-persistent kernel, loop form 5/7: BVH nodes dictionary-coded (8-bit
-                                  indices into the scene's <= 256 distinct bound values, 12 B per node) so
-                                  the whole tree sits in LDS: 1 where the split cache would be used (default:
-                                  C5 scene 29.5 -> 26.1 ms), 2 always (tests; on trees that fit plain it
-                                  only adds decoding: C3 9.6 -> 12.1 ms), 0 off */
+#define MM_OPT_DICT_NODES 20  /* BVH forms 5/7: BVH nodes dictionary-coded (8-bit indices into the scene's
+                                  <= 256 distinct bound values, 12 B per node) so the whole tree sits in LDS:
+                                  1 when the plain nodes do not fit and no explicit split size is set (default),
+                                  2 always when it fits (tests), 0 off */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
+
+/* Facts about the uploaded scene's search structures (double-valued):
+ *   MM_INFO_GRID_OK          1 if the certified grid search is available
+ *   MM_INFO_GRID_CELLS_X/Y/Z grid cells per axis
+ *   MM_INFO_GRID_GLOBAL      rects every query tests (e.g. the maze floor)
+ *   MM_INFO_GRID_BYTES       the grid image (cells, lists, records, leaf boxes)
+ *   MM_INFO_GRID_INDEX_BYTES its cells + lists part
+ *   MM_INFO_LEAN             1 if every rect has a compact record
+ *   MM_INFO_DEPTH            BVH depth (max traversal stack entries) */
+#define MM_INFO_GRID_OK          1
+#define MM_INFO_GRID_CELLS_X     2
+#define MM_INFO_GRID_CELLS_Y     3
+#define MM_INFO_GRID_CELLS_Z     4
+#define MM_INFO_GRID_GLOBAL      5
+#define MM_INFO_GRID_BYTES       6
+#define MM_INFO_GRID_INDEX_BYTES 7
+#define MM_INFO_LEAN             8
+#define MM_INFO_DEPTH            9
+int  mm_scene_info(const mm_ctx* ctx, int key, double* value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64
  * into the device buffer `dev_buf` (n_waves x 4): entry time, LDS staging

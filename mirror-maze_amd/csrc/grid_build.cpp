@@ -1,0 +1,181 @@
+// grid_build.cpp — host construction of the uniform grid the certified search
+// walks (mm_grid.h; the proof of the search is there).
+//
+// Geometry: the box of every rect corner, widened by eps = C * 2^-14 (C = the
+// largest |coordinate|, at least 1), cut into n[a] cells per axis with
+// n[a] = round(extent / s) for a cell size s = the median over the scene's
+// non-degenerate rects of their second-largest extent (the maze's wall
+// height: one cell per maze cell), clamped to 1..256 per axis.
+// Lists: a rect goes on the list of every cell its box comes within eps of;
+// rects that would sit on more than half of the cells (the maze floor) go on
+// the global list every query tests instead (at most 4); zero-length rects
+// (SKIP records: never hit) go nowhere.
+// Per rect the image also holds its compact record (rect_compact.cpp, built
+// with identity slots) and the box of the reference BVH leaf holding it --
+// the box the certificate tests.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mm_types.h"
+
+namespace mm {
+
+size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
+                           size_t* n_slow);
+
+struct GridHost {
+    float mn[3], mx[3], cell[3], inv[3];
+    int n[3];
+    uint32_t n_glob = 0;
+    uint32_t glob[4] = {0, 0, 0, 0};
+    uint32_t off_list = 0, off_recs = 0, off_box = 0, bytes = 0;
+    uint32_t n_list = 0;
+    std::vector<uint8_t> image;
+};
+
+namespace {
+
+void rect_box(const mm_rect& r, double lo[3], double hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        const double c[4] = {r.o[a], (double)r.o[a] + r.v[a], (double)r.o[a] + r.u[a],
+                             (double)r.o[a] + r.v[a] + r.u[a]};
+        lo[a] = *std::min_element(c, c + 4);
+        hi[a] = *std::max_element(c, c + 4);
+    }
+}
+
+inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+}  // namespace
+
+// Returns false (with a reason) when the scene does not suit the search:
+// rects that are not axis-aligned (SLOW records), too many rects or cells.
+bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
+                const uint32_t* idx, GridHost& g, std::string& why) {
+    if (n_rects == 0 || n_rects > 65535) { why = "rect count outside 1..65535"; return false; }
+    std::vector<uint32_t> ident(n_rects), recs;
+    for (uint32_t k = 0; k < n_rects; ++k) ident[k] = k;
+    size_t n_slow = 0;
+    build_compact_rects(rects, n_rects, ident.data(), recs, &n_slow);
+    if (n_slow) { why = "rects that are not axis-aligned"; return false; }
+    // scene box, C, eps, cell size
+    double smin[3] = {INFINITY, INFINITY, INFINITY}, smax[3] = {-INFINITY, -INFINITY, -INFINITY}, C = 1.0;
+    std::vector<double> ext2;
+    for (uint32_t k = 0; k < n_rects; ++k) {
+        double lo[3], hi[3];
+        rect_box(rects[k], lo, hi);
+        double e[3];
+        for (int a = 0; a < 3; ++a) {
+            if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) { why = "non-finite rect"; return false; }
+            smin[a] = std::min(smin[a], lo[a]);
+            smax[a] = std::max(smax[a], hi[a]);
+            C = std::max(C, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+            e[a] = hi[a] - lo[a];
+        }
+        std::sort(e, e + 3);
+        if (e[1] > 0.0) ext2.push_back(e[1]);
+    }
+    if (ext2.empty()) { why = "no rect with area"; return false; }
+    std::nth_element(ext2.begin(), ext2.begin() + ext2.size() / 2, ext2.end());
+    const double s = ext2[ext2.size() / 2];
+    const double eps = C * 0x1p-14;
+    long total = 1;
+    for (int a = 0; a < 3; ++a) {
+        const float lo = std::nextafter((float)(smin[a] - eps), -INFINITY);
+        const float hi = std::nextafter((float)(smax[a] + eps), INFINITY);
+        int n = (int)std::floor(((double)hi - lo) / s + 0.5);
+        n = std::max(1, std::min(256, n));
+        g.n[a] = n;
+        g.mn[a] = lo;
+        g.mx[a] = hi;
+        g.cell[a] = (float)(((double)hi - lo) / n);
+        g.inv[a] = 1.0f / g.cell[a];
+        total *= n;
+    }
+    if (total > (1l << 20)) { why = "more than 2^20 cells"; return false; }
+    // cell ranges of every rect (widened by eps), global rects
+    struct Span { int i0[3], i1[3]; long cover; };
+    std::vector<Span> span(n_rects);
+    std::vector<uint8_t> skip(n_rects, 0), glob(n_rects, 0);
+    std::vector<std::pair<long, uint32_t>> big;
+    for (uint32_t k = 0; k < n_rects; ++k) {
+        skip[k] = (recs[10 * (size_t)k + 9] >> 30) == 1u;
+        double lo[3], hi[3];
+        rect_box(rects[k], lo, hi);
+        Span& sp = span[k];
+        sp.cover = 1;
+        for (int a = 0; a < 3; ++a) {
+            sp.i0[a] = std::max(0, (int)std::floor((lo[a] - eps - g.mn[a]) / g.cell[a]));
+            sp.i1[a] = std::min(g.n[a] - 1, (int)std::floor((hi[a] + eps - g.mn[a]) / g.cell[a]));
+            sp.cover *= std::max(0, sp.i1[a] - sp.i0[a] + 1);
+        }
+        if (!skip[k] && sp.cover * 2 > total) big.push_back({sp.cover, k});
+    }
+    std::sort(big.begin(), big.end(), [](auto& x, auto& y) { return x.first > y.first; });
+    for (size_t i = 0; i < big.size() && i < 4; ++i) {
+        glob[big[i].second] = 1;
+        g.glob[g.n_glob++] = big[i].second;
+    }
+    // counting sort of (cell, rect)
+    std::vector<uint32_t> cnt(total + 1, 0);
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<uint32_t> cur(pass ? cnt : std::vector<uint32_t>());
+        for (uint32_t k = 0; k < n_rects; ++k) {
+            if (skip[k] || glob[k]) continue;
+            const Span& sp = span[k];
+            for (int z = sp.i0[2]; z <= sp.i1[2]; ++z)
+                for (int y = sp.i0[1]; y <= sp.i1[1]; ++y)
+                    for (int x = sp.i0[0]; x <= sp.i1[0]; ++x) {
+                        const long c = ((long)z * g.n[1] + y) * g.n[0] + x;
+                        if (pass == 0) {
+                            cnt[c + 1]++;
+                        } else {
+                            uint16_t v = (uint16_t)k;
+                            std::memcpy(&g.image[g.off_list + 2 * (size_t)cur[c]++], &v, 2);
+                        }
+                    }
+        }
+        if (pass == 0) {
+            for (long c = 0; c < total; ++c) {
+                if (cnt[c + 1] >= 1024u) { why = "a cell lists 1024 or more rects"; return false; }
+                cnt[c + 1] += cnt[c];
+            }
+            g.n_list = cnt[total];
+            if (g.n_list >= (1u << 22)) { why = "more than 2^22 list entries"; return false; }
+            g.off_list = align16(4u * (uint32_t)total);
+            g.off_recs = align16(g.off_list + 2u * g.n_list);
+            g.off_box = align16(g.off_recs + 40u * n_rects);
+            g.bytes = align16(g.off_box + 24u * n_rects);
+            g.image.assign(g.bytes, 0);
+            for (long c = 0; c < total; ++c) {
+                const uint32_t w = cnt[c] | ((cnt[c + 1] - cnt[c]) << 22);
+                std::memcpy(&g.image[4 * (size_t)c], &w, 4);
+            }
+        }
+    }
+    std::memcpy(&g.image[g.off_recs], recs.data(), 40u * (size_t)n_rects);
+    // the reference leaf box of every rect; a rect in no leaf gets an empty
+    // box, so a certificate for it always fails (the reference never tests it)
+    std::vector<float> box(6 * (size_t)n_rects);
+    for (uint32_t k = 0; k < n_rects; ++k) {
+        const float e[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, INFINITY, -INFINITY};
+        std::memcpy(&box[6 * (size_t)k], e, sizeof e);
+    }
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+        const mm_node& nd = nodes[i];
+        if (nd.count == 0) continue;
+        for (uint32_t j = 0; j < nd.count; ++j) {
+            const uint32_t k = idx[nd.left_first + j];
+            const float b[6] = {nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1], nd.mn[2], nd.mx[2]};
+            std::memcpy(&box[6 * (size_t)k], b, sizeof b);
+        }
+    }
+    std::memcpy(&g.image[g.off_box], box.data(), 24u * (size_t)n_rects);
+    return true;
+}
+
+}  // namespace mm

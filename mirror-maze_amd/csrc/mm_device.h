@@ -16,6 +16,10 @@ namespace mm {
 constexpr float kBig = 1e30f;     // shaders.metal:15, 94, 149 (IR 0x46293E5940000000)
 constexpr int kStackMax = 50;     // shaders.metal:123
 
+// Closest-hit query methods of the wave-persistent kernel (MM_OPT_TRAVERSAL):
+// BVH loop forms (mm_trace.h) and the certified grid search (mm_grid.h).
+enum : int { kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7, kFormGrid = 11 };
+
 // ---- HBM layouts ------------------------------------------------------------
 // Reference node (nodes_ref): 2 x float4 = the reference's 32-B bvh_node,
 //   a = (mn.x, mn.y, mn.z, mx.x)   b = (mx.y, mx.z, bits(left_first), bits(count))
@@ -30,6 +34,24 @@ constexpr int kStackMax = 50;     // shaders.metal:123
 // n, |v|, |u| are the per-rect subexpressions of ray_rect_intersect
 // (shaders.metal:52,60,61), computed once by k_prep_rects with the same ops.
 // Shade record: s0 = (color.rgb, is_mirror), s1 = emission (rgba).
+// Uniform grid of the certified search (mm_grid.h, built by grid_build.cpp).
+// The device image is one buffer: [cells: n_cells u32][list: u16, padded to
+// 16 B][recs: 5 x uint2 per rect][box: 3 x float2 per rect]; the byte
+// offsets of the sections let a kernel stage a prefix of it in LDS.
+struct DevGrid {
+    float mn[3], mx[3];        // grid box (scene bounds widened by eps)
+    float cell[3], inv[3];     // cell size per axis and its reciprocal
+    int n[3];                  // cells per axis
+    uint32_t n_glob;           // rects every query tests (cover > half the cells)
+    uint32_t glob[4];
+    const uint32_t* cells;     // per cell: first list entry | count << 22
+    const uint16_t* list;      // rect indices
+    const uint2* recs;         // per-rect compact records (rect_compact.cpp, FAST)
+    const float2* box;         // per rect: its reference leaf's box, (mn, mx) per axis
+    const uint4* image;        // the whole image (16-B units)
+    uint32_t off_list, off_recs, off_box, bytes;  // section offsets in bytes
+};
+
 struct DevScene {
     const float4* nodes;      // 2 * n_nodes, production layout
     const float4* nodes_ref;  // 2 * n_nodes_ref, reference layout
@@ -42,16 +64,12 @@ struct DevScene {
     uint32_t root_packed;     // count<<24 | left_first of node 0
     uint32_t fast_ok;         // scene coordinates inside the Markstein guard
     const uint2* recs;        // 5 x uint2 per BVH slot: compact rect records (rect_compact.cpp)
-    // Verified conservative search (MM_OPT_TRAVERSAL 9): `nodes` then holds the
-    // boxes expanded by cons_margin, these the exact ones and each slot's leaf box
-    const float4* nodes_exact;  // 2 * n_nodes, production layout, exact bounds
-    const float4* slot_box;     // 2 per slot: (mn.x, mx.x, mn.y, mx.y), (mn.z, mx.z, 0, 0) of its leaf
-    float cons_bound;           // |ray origin component| must be <= this for the search (else exact)
     // Dictionary-coded nodes (LDS mode 10, MM_OPT_DICT_NODES): the distinct bound
     // values (<= 256) and 3 words per production node: 8-bit indices of
     // (mn.x, mx.x, mn.y, mx.y), of (mn.z, mx.z), and the packed child word
     const float* dict_tab;      // 256 floats
     const uint32_t* dict_words; // 3 * n_nodes
+    DevGrid grid;
 };
 
 // ---- IEEE helpers (the AIR intrinsics with their IEEE meaning) -------------

@@ -1,0 +1,170 @@
+// mm_grid.h — certified grid search: the closest hit of the reference's BVH
+// walk (intersect_bvh_iterative, shaders.metal:115-156) without walking it.
+//
+// Why the answer is the reference's.  Let A be the set of rects that pass
+// ray_rect_intersect (shaders.metal:51-67) with every clause except `a < t`,
+// a* = min over A of a, attained by R* only, and L* the reference BVH leaf
+// holding R*.  If L*'s box passes intersect_aabb (shaders.metal:87-95) at
+// every t > a* -- tmax >= tmin, tmax > 0, tmin <= a* -- then the reference
+// returns (a*, R*) whatever order it visits nodes in:
+//   * t starts at 1e30 and only a rect of A can lower it, so t >= a* always,
+//     and t > a* until R* itself is accepted (a* is attained once);
+//   * every ancestor box of L* contains L*'s box, and the slab quotients
+//     RN((b - o)/d) are monotone in b, so an ancestor's [tmin, tmax]
+//     contains L*'s; each box on the root -> L* path is tested at some
+//     t > a* and passes, so L* is reached and R* is tested at t > a* and
+//     accepted; nothing in A can replace it afterwards.
+// So it suffices to find a*, R* and to know that a* is attained once.
+//
+// The search.  The scene bounds, widened by eps = C * 2^-14 (C = the largest
+// |coordinate|), are cut into a uniform grid; each cell lists every rect whose
+// box comes within eps of it; rects that cover more than half of the cells
+// (the maze floor) are tested by every query instead.  A query tests the
+// global rects, then walks the cells the ray crosses (3-D DDA) and tests each
+// cell's list, and stops once the best a found is below the exit time of the
+// current cell (or the ray leaves the grid).  Every rect of A with a <= the
+// final best is tested: its hit point P = o + a d lies within
+// delta ~ 10 u C of the rect (the rounding of the reference's bounds test,
+// u = 2^-24), and the computed crossing times put the ray at any
+// t <= (the last exit time) within eta ~ 5 u C of a visited cell, so the
+// rect comes within delta + eta << eps of a visited cell and is on its list.
+// The exact per-rect operations (the compact records of rect_compact.cpp)
+// give each rect's a, so the minimum and whether it is attained twice are
+// exact.  scripts/grid_sim.c replays every query of a C3 frame (137 M) on
+// the CPU against the reference walk: 0 differences.
+//
+// A tie, a failed leaf-box check or a ray outside the Markstein guards /
+// the grid runs the reference walk (the BVH traversal) instead.
+#pragma once
+
+#include "mm_trace.h"
+
+namespace mm {
+
+// Per-rect compact record test for the search: updates (best, bk, tie) with
+// the rect's a if it is in A (every clause of ray_rect_intersect except
+// a < t).  Records are rect_compact.cpp's FAST records, indexed by rect.
+template <typename R>
+__device__ __forceinline__ void grid_rect(const R& recs, uint32_t k, const Ray& r, float& best, uint32_t& bk,
+                                          bool& tie) {
+    const uint2 w01 = recs[5 * k + 0], w23 = recs[5 * k + 1], w45 = recs[5 * k + 2], w67 = recs[5 * k + 3],
+                w89 = recs[5 * k + 4];
+    const uint32_t meta = w89.y;
+    const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
+    const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
+    const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
+    const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
+    if (x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) && x2 >= __uint_as_float(w67.y) &&
+        x2 <= __uint_as_float(w89.x) && a > 0.1f) {
+        if (a < best) {
+            best = a;
+            bk = k;
+            tie = false;
+        } else if (a == best && k != bk) {
+            tie = true;
+        }
+    }
+}
+
+// Where the grid's arrays are read from (LDS or global memory).
+template <typename CellsT, typename ListT, typename RecsT, typename BoxT>
+struct GridView {
+    CellsT cells;  // per cell: first list entry | count << 22
+    ListT list;    // rect indices (u16)
+    RecsT recs;    // 5 x uint2 per rect
+    BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
+};
+template <typename C, typename L, typename R, typename B>
+__device__ __forceinline__ GridView<C, L, R, B> grid_view(C c, L l, R r, B b) {
+    return GridView<C, L, R, B>{c, l, r, b};
+}
+
+__device__ __forceinline__ bool grid_ray_ok(const DevGrid& g, const Ray& r) {
+    return r.o.x >= g.mn[0] && r.o.x <= g.mx[0] && r.o.y >= g.mn[1] && r.o.y <= g.mx[1] && r.o.z >= g.mn[2] &&
+           r.o.z <= g.mx[2];
+}
+
+__device__ __forceinline__ int grid_cell(const DevGrid& g, float o, int a) {
+    const int i = (int)floorf((o - g.mn[a]) * g.inv[a]);
+    return min(max(i, 0), g.n[a] - 1);
+}
+
+// The next boundary crossing on axis a from cell i: (boundary - o) * (1/d).
+__device__ __forceinline__ float grid_next(const DevGrid& g, int a, int i, bool up, float o, float y) {
+    return ((g.mn[a] + (float)(i + (up ? 1 : 0)) * g.cell[a]) - o) * y;
+}
+
+// Search + certificate.  Returns true with (t, index) = the reference's answer
+// (t = kBig when nothing is hit), false when the caller must walk the BVH.
+// Requires sc.fast_ok && ray_fast_ok(r) && grid_ray_ok.
+template <bool kStats, typename GV>
+__device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const Ray& r, float& t,
+                                            uint32_t& index, Counters& c) {
+    float best = kBig;
+    uint32_t bk = 0xFFFFFFFFu;
+    bool tie = false;
+    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect(gv.recs, g.glob[j], r, best, bk, tie);
+    const bool ux = r.d.x > 0.0f, uy = r.d.y > 0.0f, uz = r.d.z > 0.0f;
+    int ix = grid_cell(g, r.o.x, 0), iy = grid_cell(g, r.o.y, 1), iz = grid_cell(g, r.o.z, 2);
+    float tx = grid_next(g, 0, ix, ux, r.o.x, r.y.x);
+    float ty = grid_next(g, 1, iy, uy, r.o.y, r.y.y);
+    float tz = grid_next(g, 2, iz, uz, r.o.z, r.y.z);
+    uint32_t cw = gv.cells[(iz * g.n[1] + iy) * g.n[0] + ix];
+    uint32_t j = cw & 0x3FFFFFu, jend = j + (cw >> 22);
+    uint32_t cells = 1, tests = g.n_glob;
+    // One iteration: test one rect of the current cell; when the cell's list
+    // is done, step to the next cell (or stop) in the same iteration.
+    for (;;) {
+        if (j < jend) {
+            grid_rect(gv.recs, (uint32_t)gv.list[j], r, best, bk, tie);
+            ++j;
+            if (kStats) ++tests;
+        }
+        if (j >= jend) {
+            const float te = fminf(tx, fminf(ty, tz));
+            if (best < te) break;
+            if (tx == te) {
+                ix += ux ? 1 : -1;
+                if (ix < 0 || ix >= g.n[0]) break;
+                tx = grid_next(g, 0, ix, ux, r.o.x, r.y.x);
+            } else if (ty == te) {
+                iy += uy ? 1 : -1;
+                if (iy < 0 || iy >= g.n[1]) break;
+                ty = grid_next(g, 1, iy, uy, r.o.y, r.y.y);
+            } else {
+                iz += uz ? 1 : -1;
+                if (iz < 0 || iz >= g.n[2]) break;
+                tz = grid_next(g, 2, iz, uz, r.o.z, r.y.z);
+            }
+            cw = gv.cells[(iz * g.n[1] + iy) * g.n[0] + ix];
+            j = cw & 0x3FFFFFu;
+            jend = j + (cw >> 22);
+            if (kStats) ++cells;
+        }
+    }
+    if (kStats) {
+        c.visits += cells;
+        c.rtests += tests;
+    }
+    if (best == kBig) {  // A is empty: the reference finds nothing either
+        t = kBig;
+        return !tie;
+    }
+    if (tie) return false;
+    // certificate: R*'s reference leaf box passes at every t > best
+    const float2 bx = gv.box[3 * bk + 0], by = gv.box[3 * bk + 1], bz = gv.box[3 * bk + 2];
+    const float tx1 = qdiv(bx.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(bx.y - r.o.x, r.d.x, r.y.x);
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    const float ty1 = qdiv(by.x - r.o.y, r.d.y, r.y.y), ty2 = qdiv(by.y - r.o.y, r.d.y, r.y.y);
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    tmax = fminf(tmax, fmaxf(ty1, ty2));
+    const float tz1 = qdiv(bz.x - r.o.z, r.d.z, r.y.z), tz2 = qdiv(bz.y - r.o.z, r.d.z, r.y.z);
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    tmax = fminf(tmax, fmaxf(tz1, tz2));
+    if (!(tmax >= tmin && tmax > 0.0f && tmin <= best)) return false;
+    t = best;
+    index = bk;
+    return true;
+}
+
+}  // namespace mm

@@ -32,13 +32,6 @@ struct TileJob {
     // ticks (100 MHz).  Null = off.
     unsigned long long* wave_ts = nullptr;
     uint32_t wave_ts_cap = 0;
-    uint32_t fair = 0;   // MM_OPT_FAIR bits (wave-persistent kernel scheduling)
-    uint32_t grab = 1;   // 64-path chunks claimed per atomic (MM_OPT_GRAB)
-    // MM_OPT_CHUNK_ORDER (wave-persistent kernel): queue position q runs
-    // 64-path chunk order[q] (a permutation; null = identity), and cost[chunk]
-    // receives the chunk's duration in wall_clock64() ticks (null = off).
-    const uint32_t* order = nullptr;
-    uint32_t* cost = nullptr;
     // Multi-frame launch (mm_trace_tile_frames; wave-persistent kernel, fused
     // resolve): the queue holds n_frames frames' chunks back to back; frame f
     // uses RNG frame e.frame + f and writes out + f * w * h.
@@ -59,40 +52,15 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
                              unsigned long long* stats_dev, uint32_t* err, bool count_stats,
                              const MegaOpts& o, hipStream_t s);
 
-// Throughput mode, wave-persistent megakernel: resident blocks, waves pull
-// 64-path chunks from work[0]; work[0..1] must be zero at launch and are left
-// zero by the kernel itself (the last wave re-zeroes them).
+// Throughput mode, wave-persistent megakernel: resident 1024-thread blocks,
+// waves pull 64-path chunks from work[0]; work[0..1] must be zero at launch
+// and are left zero by the kernel itself (the last wave re-zeroes them).
+// lds_mode / form: trace_kernels.hip (k_trace_wavepersist); returns
+// hipErrorInvalidValue for a pair that is not instantiated.
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
-                                    int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
-                                    int loop_form, hipStream_t s);
-
-// Longest-first chunk order from the previous launch's chunk durations
-// (chunk_order.hip): order = chunks sorted by descending duration in
-// 1/16-octave bins (ties in any order).  tmp: 1024 u32 of scratch, zeroed here.
-hipError_t launch_chunk_order(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* tmp, hipStream_t s);
-
-// Throughput mode, block-synchronous bounces with ray compaction
-// (trace_block.hip, MM_OPT_BLOCKSYNC): 1024-thread blocks, BVH in LDS.
-size_t blocksync_lds_bytes(const DevScene& sc, uint32_t block);
-hipError_t launch_trace_blocksync(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
-                                  uint32_t* err, uint32_t* work, bool count_stats, hipStream_t s);
-
-struct PersistOpts {
-    int lds_mode = 1;          // 0 nodes via cache, 1 nodes in LDS, 3 nodes + compact rects in LDS
-    uint32_t block = 1024;
-    uint32_t min_waves = 8;    // launch-bounds occupancy target (waves per SIMD)
-    uint32_t threshold = 32;   // keep stepping traversals while > threshold lanes traverse
-};
-
-// (block, min_waves) pairs launch_trace_persist is compiled for.
-bool persist_instantiated(uint32_t block, uint32_t min_waves);
-
-// Throughput mode, lane-refill persistent megakernel (trace_persist.hip).
-// `work` is a device u32 path counter (zeroed by the launcher).
-hipError_t launch_trace_persist(const DevScene& sc, const TileJob& job, float4* samples,
-                                unsigned long long* stats_dev, uint32_t* err, uint32_t* work, bool count_stats,
-                                const PersistOpts& o, hipStream_t s);
+                                    int lds_mode, int form, hipStream_t s);
+size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
 
 // ---- wavefront pipeline (trace_wave.hip) ---------------------------------------
 struct WaveState {
@@ -128,9 +96,6 @@ hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, ui
 hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,
                                 float4* out, hipStream_t s);
 hipError_t launch_quantize(const float4* in, uint32_t* out, size_t n, hipStream_t s);
-
-// One-wave no-op ahead of a trace launch (MM_OPT_TAIL_GATE, trace_kernels.hip).
-hipError_t launch_tail_gate(hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);

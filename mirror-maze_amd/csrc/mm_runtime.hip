@@ -23,6 +23,17 @@ using namespace mm;
 namespace mm {
 size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
                            size_t* n_slow);
+struct GridHost {
+    float mn[3], mx[3], cell[3], inv[3];
+    int n[3];
+    uint32_t n_glob = 0;
+    uint32_t glob[4] = {0, 0, 0, 0};
+    uint32_t off_list = 0, off_recs = 0, off_box = 0, bytes = 0;
+    uint32_t n_list = 0;
+    std::vector<uint8_t> image;
+};
+bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
+                const uint32_t* idx, GridHost& g, std::string& why);
 }
 
 struct mm_ctx {
@@ -37,18 +48,18 @@ struct mm_ctx {
     uint32_t root_packed = 0;
     bool fast_ok = false;
     uint32_t depth = 0;         // tree depth = max traversal stack entries
-    bool stack16_ok = false;    // every node packs into 16 bits (count < 16, left_first < 4096)
     float4* d_geo = nullptr;
     float4* d_shade = nullptr;
     uint2* d_recs = nullptr;    // compact leaf-ordered rect records
     size_t n_fast_recs = 0;
-    bool lean_ok = false;       // no SLOW rect records (loop forms 7, 9)
+    bool lean_ok = false;       // no SLOW rect records (loop form 7, grid search)
     float* d_dict_tab = nullptr;       // dictionary-coded nodes (mode 10): 256 values
     uint32_t* d_dict_words = nullptr;  // 3 words per production node
     bool dict_ok = false;
-    float4* d_nodes_cons = nullptr;  // production layout, boxes expanded by the search margin (form 9)
-    float4* d_slot_box = nullptr;    // per BVH slot: its leaf's exact box (form 9 verification)
-    float cons_bound = 0.0f;         // |coordinate| bound of the scene (form 9 ray guard)
+    uint8_t* d_grid = nullptr;  // certified grid search (grid_build.cpp, mm_grid.h)
+    DevGrid grid{};
+    bool grid_ok = false;
+    std::string grid_why;
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
     bool has_scene = false;
@@ -75,38 +86,16 @@ struct mm_ctx {
     float last_ms = 0.0f;
     uint32_t last_launches = 0;
     int pipe = MM_PIPE_AUTO;
-    bool opt_lds = true;
-    uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto size, else KB
-    bool opt_cold_lds = false;      // park T and L in LDS during traversal
-    int opt_glob_rects = 2;         // compact rect records via L1/L2: 0 never, 1 whenever not in LDS,
-                                    // 2 (auto) with the split node cache only (measured: C5 +3 %, C3 -2 %)
-    uint32_t opt_block = 0;  // 0 = auto: 512 with LDS-staged nodes, 256 otherwise
-    // Megakernel form (measured on C3, profiles/r01_ab_*.txt): wave-persistent
-    // 1024-thread blocks at <= 64 VGPRs (8 waves/SIMD) with the BVH in LDS.
-    int opt_persist = 2;         // 0 one thread per path, 1 lane refill, 2 wave-persistent
-    uint32_t opt_min_waves = 8;  // wave-persistent launch bound (waves per SIMD)
-    int opt_ww = -1;             // traversal loop: -1 auto (5 at 1024/8, else 0), 0 if-if, 1 while-while,
-                                 // 5 leaf+interior per iteration, 8/16/32 leaf batch
-    int opt_lds_rects = 1;       // compact rect records in LDS next to the BVH when they fit
-    int opt_lds_stack = 0;       // u16 stack: 1 in LDS with LDS nodes only, 2 + rect records via L1/L2 (form 5),
-                                 // 3 in scratch beside LDS nodes + records (form 5)
-    uint32_t opt_threshold = 32;
-    bool opt_fuse = true;        // resolve fused into the wave-persistent kernel when 64 % spp == 0
-    bool opt_tail_gate = false;  // one-wave no-op ahead of each trace launch (contexts sharing the GPU)
-    uint32_t opt_fair = 0;       // MM_OPT_FAIR: issue priority for waves behind the mean chunk count
-    uint32_t opt_grab = 1;       // chunks per work-counter atomic
-    bool opt_blocksync = false;  // block-synchronous bounces with ray compaction (trace_block.hip)
-    uint32_t opt_reserve_cus = 0;  // MM_OPT_RESERVE_CUS
-    uint32_t opt_dict = 1;         // MM_OPT_DICT_NODES: 0 off, 1 instead of the split cache (default), 2 always
-    uint32_t opt_chunk_order = 0;  // MM_OPT_CHUNK_ORDER: 0 pixel order, 1 longest first (previous launch)
-    // longest-first chunk order (chunk_order.hip): durations of the last launch
-    // of the tile `order_key` describes, the permutation sorted from them
-    uint32_t* d_cost = nullptr;
-    uint32_t* d_order = nullptr;
-    uint32_t* d_order_tmp = nullptr;   // 1024 u32: histogram + cursors
-    size_t cost_cap = 0, order_cap = 0, order_tmp_cap = 0;
-    uint32_t order_key[8] = {};
-    bool order_ready = false;
+    // options (include/mm_api.h MM_OPT_*); defaults = the measured fastest
+    bool opt_lds = true;            // stage scene data in LDS where it fits
+    uint32_t opt_block = 0;         // k_trace_mega block size (0 = auto)
+    int opt_persist = 2;            // 0 one thread per path (k_trace_mega), 2 wave-persistent
+    int opt_ww = -1;                // loop form: -1 auto, 0, 5, 7 (BVH), 11 (grid search)
+    int opt_lds_rects = 1;          // compact rect records in LDS beside the nodes when they fit
+    uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto, else KB (always)
+    bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
+    uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
+    uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
@@ -146,9 +135,7 @@ DevScene dev_scene(const mm_ctx* c) {
     s.fast_ok = c->fast_ok ? 1u : 0u;
     s.geo = c->d_geo;
     s.recs = c->d_recs;
-    s.nodes_exact = c->d_nodes;
-    s.slot_box = c->d_slot_box;
-    s.cons_bound = c->cons_bound;
+    s.grid = c->grid;
     s.dict_tab = c->d_dict_tab;
     s.dict_words = c->d_dict_words;
     s.shade = c->d_shade;
@@ -161,8 +148,8 @@ DevScene dev_scene(const mm_ctx* c) {
 void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_nodes_ref); (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
-    (void)hipFree(c->d_nodes_cons); (void)hipFree(c->d_slot_box);
-    c->d_nodes_cons = nullptr; c->d_slot_box = nullptr;
+    (void)hipFree(c->d_grid);
+    c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false;
     (void)hipFree(c->d_dict_tab); (void)hipFree(c->d_dict_words);
     c->d_dict_tab = nullptr; c->d_dict_words = nullptr; c->dict_ok = false;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
@@ -313,7 +300,6 @@ void mm_destroy(mm_ctx* c) {
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave);
-    (void)hipFree(c->d_cost); (void)hipFree(c->d_order); (void)hipFree(c->d_order_tmp);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -353,66 +339,52 @@ int mm_set_option(mm_ctx* c, int key, int value) {
     if (!c) return MM_ERR_INVALID;
     switch (key) {
         case MM_OPT_LDS_NODES: c->opt_lds = value != 0; return MM_OK;
-        case MM_OPT_PERSIST:
-            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "persist must be 0, 1 or 2");
-            c->opt_persist = value;
-            return MM_OK;
-        case MM_OPT_THRESHOLD:
-            if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "threshold must be 0..63");
-            c->opt_threshold = (uint32_t)value;
-            return MM_OK;
-        case MM_OPT_LDS_STACK:
-            if (value < 0 || value > 3) return fail(c, MM_ERR_INVALID, "lds stack must be 0..3");
-            c->opt_lds_stack = value;
-            return MM_OK;
-        case MM_OPT_TRAVERSAL:
-            if (value < -1 || (value > 9 && value != 16 && value != 32))
-                return fail(c, MM_ERR_INVALID, "traversal loop form must be -1, 0-9, 16 or 32");
-            c->opt_ww = value;
-            return MM_OK;
-        case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
-        case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
-        case MM_OPT_TAIL_GATE: c->opt_tail_gate = value != 0; return MM_OK;
-        case MM_OPT_BLOCKSYNC: c->opt_blocksync = value != 0; return MM_OK;
-        case MM_OPT_DICT_NODES:
-            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
-            c->opt_dict = (uint32_t)value;
-            return MM_OK;
-        case MM_OPT_RESERVE_CUS:
-            if (value < 0 || value > 128) return fail(c, MM_ERR_INVALID, "reserved CUs must be 0..128");
-            c->opt_reserve_cus = (uint32_t)value;
-            return MM_OK;
-        case MM_OPT_CHUNK_ORDER:
-            if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "chunk order must be 0 or 1");
-            c->opt_chunk_order = (uint32_t)value;
-            c->order_ready = false;
-            return MM_OK;
-        case MM_OPT_GRAB:
-            if (value < 1 || value > 16) return fail(c, MM_ERR_INVALID, "grab must be 1..16");
-            c->opt_grab = (uint32_t)value;
-            return MM_OK;
-        case MM_OPT_FAIR:
-            if (value < 0 || value > 1) return fail(c, MM_ERR_INVALID, "fair must be 0 or 1");
-            c->opt_fair = (uint32_t)value;
-            return MM_OK;
-        case MM_OPT_COLD_LDS: c->opt_cold_lds = value != 0; return MM_OK;
-        case MM_OPT_GLOBAL_RECTS:
-            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "global rects must be 0, 1 or 2");
-            c->opt_glob_rects = value;
-            return MM_OK;
-        case MM_OPT_LDS_SPLIT:
-            if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
-            c->opt_lds_split = (uint32_t)value;
-            return MM_OK;
-        case MM_OPT_MIN_WAVES:
-            if (value != 1 && value != 6 && value != 8) return fail(c, MM_ERR_INVALID, "min waves must be 1, 6 or 8");
-            c->opt_min_waves = (uint32_t)value;
-            return MM_OK;
         case MM_OPT_BLOCK:
             if (value < 64 || value > 1024 || value % 64) return fail(c, MM_ERR_INVALID, "block must be 64..1024, x64");
             c->opt_block = (uint32_t)value;
             return MM_OK;
+        case MM_OPT_PERSIST:
+            if (value != 0 && value != 2) return fail(c, MM_ERR_INVALID, "persist must be 0 or 2");
+            c->opt_persist = value;
+            return MM_OK;
+        case MM_OPT_TRAVERSAL:
+            if (value != -1 && value != 0 && value != 5 && value != 7 && value != 11)
+                return fail(c, MM_ERR_INVALID, "traversal must be -1 (auto), 0, 5, 7 or 11 (grid search)");
+            c->opt_ww = value;
+            return MM_OK;
+        case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
+        case MM_OPT_LDS_SPLIT:
+            if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
+            c->opt_lds_split = (uint32_t)value;
+            return MM_OK;
+        case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
+        case MM_OPT_RESERVE_CUS:
+            if (value < 0 || value > 128) return fail(c, MM_ERR_INVALID, "reserved CUs must be 0..128");
+            c->opt_reserve_cus = (uint32_t)value;
+            return MM_OK;
+        case MM_OPT_DICT_NODES:
+            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
+            c->opt_dict = (uint32_t)value;
+            return MM_OK;
         default: return fail(c, MM_ERR_INVALID, "unknown option");
+    }
+}
+
+int mm_scene_info(const mm_ctx* c, int key, double* value) {
+    if (!c || !value) return MM_ERR_INVALID;
+    if (!c->has_scene) return MM_ERR_NO_SCENE;
+    const DevGrid& g = c->grid;
+    switch (key) {
+        case MM_INFO_GRID_OK: *value = c->grid_ok ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_GRID_CELLS_X: *value = g.n[0]; return MM_OK;
+        case MM_INFO_GRID_CELLS_Y: *value = g.n[1]; return MM_OK;
+        case MM_INFO_GRID_CELLS_Z: *value = g.n[2]; return MM_OK;
+        case MM_INFO_GRID_GLOBAL: *value = g.n_glob; return MM_OK;
+        case MM_INFO_GRID_BYTES: *value = g.bytes; return MM_OK;
+        case MM_INFO_GRID_INDEX_BYTES: *value = g.off_recs; return MM_OK;
+        case MM_INFO_LEAN: *value = c->lean_ok ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_DEPTH: *value = c->depth; return MM_OK;
+        default: return MM_ERR_INVALID;
     }
 }
 
@@ -452,12 +424,10 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     };
     const uint32_t n_prod = 2 + 2 * (uint32_t)pair_old.size();
     std::vector<float4> packed(2 * (size_t)n_prod, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    bool stack16 = true;
     for (size_t q = 0; q < pair_old.size(); ++q)
         for (uint32_t k = 0; k < 2; ++k) {
             const mm_node& nd = nodes[pair_old[q] + k];
             const uint32_t pk = pack(nd);
-            if ((pk >> 24) >= 16u || (pk & 0xFFFFFFu) >= 4096u) stack16 = false;
             float pkf;
             std::memcpy(&pkf, &pk, 4);
             const size_t i = 2 + 2 * q + k;
@@ -496,30 +466,6 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         }
         dict.resize(256, 0.0f);
     }
-    // Verified conservative search (form 9): boxes expanded outward by
-    // E = C * 2^-14, C = the scene's largest |coordinate| (>= 64x the rounding
-    // bound of mm_trace.h: traverse_cons), and each slot's exact leaf box.
-    float cbound = 1.0f;
-    for (uint32_t i = 0; i < n_nodes; ++i)
-        for (int a = 0; a < 3; ++a) cbound = std::max(cbound, std::max(std::fabs(nodes[i].mn[a]), std::fabs(nodes[i].mx[a])));
-    const double margin = (double)cbound * 0x1p-14;
-    auto dn = [&](float x) { return std::nextafter((float)((double)x - margin), -INFINITY); };
-    auto up = [&](float x) { return std::nextafter((float)((double)x + margin), INFINITY); };
-    std::vector<float4> packed_cons(packed);
-    for (size_t i = 4; i < packed_cons.size(); i += 2) {
-        float4& a = packed_cons[i];
-        float4& b = packed_cons[i + 1];
-        a = make_float4(dn(a.x), up(a.y), dn(a.z), up(a.w));
-        b = make_float4(dn(b.x), up(b.y), b.z, b.w);
-    }
-    std::vector<float4> slot_box(2 * (size_t)n_rects, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    for (uint32_t i = 0; i < n_nodes; ++i)
-        if (nodes[i].count > 0)
-            for (uint32_t j = 0; j < nodes[i].count; ++j) {
-                const uint32_t sl = nodes[i].left_first + j;
-                slot_box[2 * (size_t)sl] = make_float4(nodes[i].mn[0], nodes[i].mx[0], nodes[i].mn[1], nodes[i].mx[1]);
-                slot_box[2 * (size_t)sl + 1] = make_float4(nodes[i].mn[2], nodes[i].mx[2], 0.0f, 0.0f);
-            }
     bool fast = true;
     for (uint32_t i = 0; i < n_nodes && fast; ++i)
         for (int a = 0; a < 3; ++a) fast = fast && coord_ok(nodes[i].mn[a]) && coord_ok(nodes[i].mx[a]);
@@ -549,12 +495,29 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     // mm_node is exactly two float4: (mn.xyz, mx.x) (mx.yz, left_first, count)
     HIPC(c, hipMemcpyAsync(c->d_nodes_ref, nodes, n_nodes * sizeof(mm_node), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_nodes, packed.data(), packed.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMalloc((void**)&c->d_nodes_cons, packed_cons.size() * sizeof(float4)));
-    HIPC(c, hipMemcpyAsync(c->d_nodes_cons, packed_cons.data(), packed_cons.size() * sizeof(float4),
-                           hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMalloc((void**)&c->d_slot_box, slot_box.size() * sizeof(float4)));
-    HIPC(c, hipMemcpyAsync(c->d_slot_box, slot_box.data(), slot_box.size() * sizeof(float4), hipMemcpyHostToDevice,
-                           c->stream));
+    // certified grid search (mm_grid.h): needs the Markstein guards and axis-aligned rects
+    GridHost gh;
+    std::string gwhy;
+    const bool grid_ok = fast && n_slow == 0 && build_grid(rects, n_rects, nodes, n_nodes, idx, gh, gwhy);
+    if (!fast) gwhy = "scene coordinates outside the exact-division guards";
+    if (fast && n_slow) gwhy = "rects that are not axis-aligned";
+    DevGrid dg{};
+    if (grid_ok) {
+        HIPC(c, hipMalloc((void**)&c->d_grid, gh.bytes));
+        HIPC(c, hipMemcpyAsync(c->d_grid, gh.image.data(), gh.bytes, hipMemcpyHostToDevice, c->stream));
+        for (int a = 0; a < 3; ++a) {
+            dg.mn[a] = gh.mn[a]; dg.mx[a] = gh.mx[a]; dg.cell[a] = gh.cell[a]; dg.inv[a] = gh.inv[a];
+            dg.n[a] = gh.n[a];
+        }
+        dg.n_glob = gh.n_glob;
+        for (int i = 0; i < 4; ++i) dg.glob[i] = gh.glob[i];
+        dg.cells = reinterpret_cast<const uint32_t*>(c->d_grid);
+        dg.list = reinterpret_cast<const uint16_t*>(c->d_grid + gh.off_list);
+        dg.recs = reinterpret_cast<const uint2*>(c->d_grid + gh.off_recs);
+        dg.box = reinterpret_cast<const float2*>(c->d_grid + gh.off_box);
+        dg.image = reinterpret_cast<const uint4*>(c->d_grid);
+        dg.off_list = gh.off_list; dg.off_recs = gh.off_recs; dg.off_box = gh.off_box; dg.bytes = gh.bytes;
+    }
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     if (dict_ok) {
         HIPC(c, hipMalloc((void**)&c->d_dict_tab, 256 * sizeof(float)));
@@ -570,10 +533,11 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     c->n_nodes = n_prod;
     c->root_packed = pack(nodes[0]);
     c->depth = depth;
-    c->stack16_ok = stack16 && (c->root_packed >> 24) < 16u && (c->root_packed & 0xFFFFFFu) < 4096u;
     c->fast_ok = fast;
-    c->cons_bound = cbound;
     c->lean_ok = n_slow == 0;
+    c->grid = dg;
+    c->grid_ok = grid_ok;
+    c->grid_why = grid_ok ? std::string() : gwhy;
     c->dict_ok = dict_ok;
     c->has_scene = true;
     return MM_OK;
@@ -675,6 +639,64 @@ int mm_read_framebuffer(mm_ctx* c, float* rgba, uint8_t* rgba8) {
 
 namespace {
 
+// Loop form and LDS mode of the wave-persistent kernel (trace_kernels.hip).
+// 1024-thread blocks at 8 waves per SIMD -> two blocks per CU -> 80 KB of LDS
+// each.  Auto (MM_OPT_TRAVERSAL -1): the certified grid search when the scene
+// allows it (C3 ...), else the lean BVH loop (form 7) when every rect has a
+// compact record, else form 5.  BVH data placement: nodes + records in LDS
+// when both fit; nodes in LDS, records through L1/L2 when only the nodes do;
+// otherwise dictionary-coded nodes (mode 10) when they fit, else the top of
+// the tree (split cache, mode 6).  An explicit MM_OPT_LDS_SPLIT > 1 always
+// uses the split cache of that size; MM_OPT_DICT_NODES 2 always uses the
+// dictionary when it fits; MM_OPT_LDS_NODES 0 stages nothing.
+int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
+    const size_t budget = 80 * 1024;
+    const bool auto_form = c->opt_ww < 0;
+    form = auto_form ? (c->grid_ok ? kFormGrid : (c->lean_ok ? kFormLean : kFormLeafInterior)) : c->opt_ww;
+    if (form == kFormGrid) {
+        if (!c->grid_ok)
+            return fail(c, MM_ERR_UNSUPPORTED, "grid search unavailable for this scene: " + c->grid_why);
+        if (c->opt_lds && c->grid.bytes <= budget) { mode = 11; return MM_OK; }
+        if (c->opt_lds && c->grid.off_recs <= budget) { mode = 12; return MM_OK; }
+        if (!auto_form || !c->opt_lds) { mode = 13; return MM_OK; }
+        // the index does not fit LDS: auto takes the BVH (nodes in LDS or cached), which is not
+        // measured against the all-global grid
+        form = c->lean_ok ? kFormLean : kFormLeafInterior;
+    }
+    if (form == kFormLean && !c->lean_ok) {
+        if (!auto_form) return fail(c, MM_ERR_UNSUPPORTED, "loop form 7 needs compact records for every rect");
+        form = kFormLeafInterior;
+    }
+    const size_t nodes_b = 2 * (size_t)c->n_nodes * sizeof(float4);
+    const size_t recs_b = 40 * (size_t)c->n_rects;
+    const size_t dict_b = 256 * sizeof(float) + 12 * (size_t)c->n_nodes;
+    const bool dict_fits = c->opt_dict && c->dict_ok && dict_b <= budget;
+    if (!c->opt_lds) {
+        mode = 0;
+    } else if (c->opt_dict == 2 && dict_fits) {
+        mode = 10;
+    } else if (c->opt_lds_split > 1) {
+        mode = 6;
+        sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, (size_t)c->opt_lds_split * 1024 /
+                                                                              sizeof(float4)) & ~3u;
+    } else if (nodes_b <= budget) {
+        mode = (c->opt_lds_rects && nodes_b + recs_b <= budget) ? 3 : (form == kFormIfIf ? 1 : 7);
+    } else if (dict_fits) {
+        mode = 10;
+    } else if (c->opt_lds_split == 1) {
+        mode = 6;
+        sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
+    } else {
+        mode = 0;
+    }
+    if (form == kFormLean && mode == 0) form = kFormLeafInterior;
+    // the lean form with the split cache measured slower (C5 scene 30.6 vs 29.4 ms): auto keeps form 5 there
+    if (auto_form && form == kFormLean && mode == 6) form = kFormLeafInterior;
+    if (form == kFormIfIf && mode != 1 && mode != 3)
+        return fail(c, MM_ERR_UNSUPPORTED, "loop form 0 is built for nodes in LDS only (LDS modes 1, 3)");
+    return MM_OK;
+}
+
 int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_frames, uint32_t x0, uint32_t y0,
                     uint32_t w, uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
     if (!c) return MM_ERR_INVALID;
@@ -695,15 +717,14 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     const uint64_t row_paths = (uint64_t)w * e->spp;
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
-    const bool fuse = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_ww != 4 && c->opt_ww != 6 &&
-                      c->opt_fuse && 64 % e->spp == 0;
+    const bool fuse = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_fuse && 64 % e->spp == 0;
     const uint64_t batch_paths = fuse ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
     if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
     if (n_frames > 1) {
         // several frames in one launch: the wave-persistent kernel's queue with the fused resolve
-        if (!fuse || c->opt_blocksync)
+        if (!fuse)
             return fail(c, MM_ERR_UNSUPPORTED, "mm_trace_tile_frames: needs the wave-persistent kernel with the "
                                                "fused resolve (64 % spp == 0)");
         if (e->flags & MM_EXT_ACCUMULATE)
@@ -734,14 +755,10 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.view_w = W;
         job.fuse = fuse ? 1u : 0u;
         job.wave_ts = c->d_wave_ts;
-        job.fair = c->opt_fair;
-        job.grab = c->opt_grab;
         job.wave_ts_cap = c->wave_ts_cap;
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
         job.reserve_cus = c->opt_reserve_cus;
-        uint32_t sort_chunks = 0;  // > 0: queue the longest-first sort of this launch's chunk durations
-        if (c->opt_tail_gate) HIPC(c, launch_tail_gate(c->stream));
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
         if (wave) {
@@ -763,105 +780,14 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                 launches += 2;
             }
             launches += 1;
-        } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_blocksync &&
-                   blocksync_lds_bytes(dev_scene(c), 1024) <= 80 * 1024) {
-            HIPC(c, launch_trace_blocksync(dev_scene(c), job, c->d_samples, c->d_aux,
-                                           reinterpret_cast<uint32_t*>(c->d_aux + 4),
-                                           reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, c->stream));
         } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
-            const uint32_t block = c->opt_block ? c->opt_block : 1024u;
-            const bool inst = (block == 256 && c->opt_min_waves == 8) || (block == 512 && c->opt_min_waves >= 6) ||
-                              (block == 768 && c->opt_min_waves == 6) ||
-                              (block == 1024 && (c->opt_min_waves == 1 || c->opt_min_waves == 8));
-            if (!inst)
-                return fail(c, MM_ERR_UNSUPPORTED, "wave-persistent kernel: block/min-waves pair not instantiated "
-                                                   "(256/8, 512/6, 512/8, 1024/1, 1024/8)");
-            // loop form: auto = leaf+interior per iteration (measured 10.35 vs 11.06 ms on C3,
-            // profiles/r01_ab_leafinterior.txt) where it is instantiated, its lean form (7)
-            // when the scene allows (below), else if-if
-            int ww = c->opt_ww >= 0 ? c->opt_ww
-                                    : ((block == 1024 && c->opt_min_waves == 8 && !c->opt_cold_lds) ? 5 : 0);
-            const uint32_t slots = std::max(1u, c->depth);
-            // LDS per block that keeps the launch-bound occupancy (min_waves per SIMD, 4 SIMDs):
-            // 1024/8 and 768/6 -> 2 blocks per CU -> 80 KB each
-            const size_t lds_budget = std::min<size_t>(160 * 1024, (size_t)(160 * 1024) * block /
-                                                                       (std::max(1u, c->opt_min_waves) * 256u));
-            const size_t lds_total = 2 * (size_t)c->n_nodes * sizeof(float4) + (size_t)slots * block * 2;
-            const bool stack_fits = c->opt_lds_stack && c->stack16_ok && lds_total <= lds_budget;
-            const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
-            const bool rects_fit = c->opt_lds_rects && lds_rects <= lds_budget;
-            int mode = lds_fits ? (rects_fit ? 3 : (stack_fits && ww != 4 && ww != 6 ? 2 : 1)) : 0;
-            const size_t lds_cold = 2 * (size_t)c->n_nodes * sizeof(float4) + 24 * (size_t)block;
-            if (lds_fits && c->opt_cold_lds && ww == 0 && lds_cold <= lds_budget)
-                mode = 5;
-            if (mode == 1 && (ww == 0 || ww == 5 || ww == 7 || ww == 9) && c->opt_glob_rects == 1) mode = 7;
-            // LDS stack beside the nodes, compact rect records through L1/L2 (loop form 5)
-            if (lds_fits && ww == 5 && c->opt_lds_stack == 2 && c->stack16_ok && block == 1024 &&
-                c->opt_min_waves == 8 && lds_total <= lds_budget)
-                mode = 8;
-            // u16 stack entries in scratch beside LDS nodes + records (loop form 5)
-            if (mode == 3 && ww == 5 && c->opt_lds_stack == 3 && c->stack16_ok && block == 1024 &&
-                c->opt_min_waves == 8)
-                mode = 9;
+            int form = 0, mode = 0;
             DevScene sc = dev_scene(c);
-            if (c->opt_lds && (ww == 0 || ww == 2 || ww == 3 || ww == 4 || ww == 5 || ww == 6 || ww == 7 || ww == 9) &&
-                (c->opt_lds_split > 1 || (!lds_fits && c->opt_lds_split == 1))) {
-                // nodes exceed the LDS budget (or an explicit cache size is set):
-                // cache the top of the breadth-first array
-                const size_t budget = c->opt_lds_split == 1 ? lds_budget
-                                                            : (size_t)c->opt_lds_split * 1024;
-                sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
-                mode = ((ww == 0 || ww == 5 || ww == 7 || ww == 9) && c->opt_glob_rects != 0) ? 6 : 4;
-            }
-            // dictionary-coded nodes, all in LDS (mode 10): instead of the split cache (1) or always (2)
-            const size_t lds_dict = 256 * sizeof(float) + 12 * (size_t)c->n_nodes;
-            if (c->opt_dict && c->dict_ok && (ww == 5 || ww == 7) && block == 1024 && c->opt_min_waves == 8 &&
-                lds_dict <= lds_budget && (c->opt_dict == 2 || mode == 6 || mode == 4))
-                mode = 10;
-            // the lean and verified-search forms need compact records for every leaf (modes 3,
-            // 6, 7) and a lean scene (no SLOW records); auto prefers the lean form
-            // (C3 10.40 -> 9.56 ms, profiles/r01_ab_lean.txt)
-            const bool lean_fits = c->lean_ok && block == 1024 && c->opt_min_waves == 8 &&
-                                   (mode == 3 || mode == 6 || mode == 7 || mode == 10);
-            // (auto: not with the split node cache, where it measured 30.6 vs 29.4 ms on the C5 scene)
-            if (c->opt_ww < 0 && ww == 5 && lean_fits && mode != 6) ww = 7;
-            if ((ww == 7 || ww == 9) && !lean_fits) ww = 5;
-            if (ww == 9) sc.nodes = c->d_nodes_cons;  // the search's expanded boxes (LDS and global)
-            // longest-first chunk order: queue the previous launch's sort for a tile of the same
-            // geometry (a frame that is one launch), record this launch's chunk durations
-            const uint32_t n_chunks = (job.w * job.h * job.e.spp + 63u) / 64u;
-            const bool ordered = c->opt_chunk_order && ww != 4 && ww != 6 && rows_per_batch >= h;
-            if (ordered) {
-                const uint32_t key[8] = {job.x0, job.y0, job.w, job.h, job.y_stride, job.view_w, job.e.spp, 1u};
-                if (!std::equal(key, key + 8, c->order_key)) {
-                    std::copy(key, key + 8, c->order_key);
-                    c->order_ready = false;
-                }
-                if ((rc = ensure(c, c->d_cost, c->cost_cap, n_chunks))) return rc;
-                if ((rc = ensure(c, c->d_order, c->order_cap, n_chunks))) return rc;
-                if ((rc = ensure(c, c->d_order_tmp, c->order_tmp_cap, 1024))) return rc;
-                job.order = c->order_ready ? c->d_order : nullptr;
-                job.cost = c->d_cost;
-            }
+            if ((rc = choose_wavepersist(c, sc, form, mode))) return rc;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
-                                             reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, slots,
-                                             block, c->opt_min_waves, ww, c->stream));
-            sort_chunks = ordered ? n_chunks : 0u;
-        } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 1) {
-            PersistOpts po;
-            po.block = c->opt_block ? c->opt_block : 1024u;
-            po.min_waves = c->opt_min_waves;
-            if (!persist_instantiated(po.block, po.min_waves))
-                return fail(c, MM_ERR_UNSUPPORTED, "lane-refill kernel: block/min-waves pair not instantiated "
-                                                   "(1024/8, 1024/1, 512/6)");
-            const size_t lds_rects = 2 * (size_t)c->n_nodes * sizeof(float4) + 40 * (size_t)c->n_rects;
-            const bool rects_fit = c->opt_lds_rects && lds_rects <= (size_t)(160 * 1024) * po.block / 2048;
-            po.lds_mode = lds_fits ? (rects_fit ? 3 : 1) : 0;
-            po.threshold = c->opt_threshold;
-            HIPC(c, launch_trace_persist(dev_scene(c), job, c->d_samples, c->d_aux,
-                                         reinterpret_cast<uint32_t*>(c->d_aux + 4),
-                                         reinterpret_cast<uint32_t*>(c->d_aux + 5), want_stats, po, c->stream));
+                                             reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
+                                             c->stream));
         } else {
             MegaOpts mo;
             mo.reference = c->pipe == MM_PIPE_REFERENCE;
@@ -871,11 +797,6 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                       reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
         }
         if ((rc = prof_mark(c))) return rc;
-        if (sort_chunks) {  // after the trace kernel's event pair: the sort is not trace time
-            HIPC(c, launch_chunk_order(c->d_cost, sort_chunks, c->d_order, c->d_order_tmp, c->stream));
-            c->order_ready = true;
-            launches += 2;
-        }
         if (fuse) {
             launches += 1;
             continue;

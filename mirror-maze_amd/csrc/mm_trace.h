@@ -4,21 +4,24 @@
 // Operation order follows src/shaders.ir; oracle/mm_oracle.c is the CPU
 // statement the parity tests compare against, bit for bit.
 //
-// Two traversals are provided:
-//   traverse_reference  the straight statement (IEEE division everywhere);
-//                       kept as MM_PIPE_REFERENCE for A/B measurement.
-//   traverse<kFast>     the production path.  With kFast every slab division
-//                       (bound - o) / d uses a per-ray correctly rounded
-//                       reciprocal y = RN(1/d) and Markstein's correction
-//                           q = a*y;  r = fma(-q, d, a);  q' = fma(r, y, q)
-//                       which equals RN(a/d) when no under/overflow occurs
-//                       (Markstein 1990; Cornea-Hasegan, Golliver, Markstein
-//                       1999).  scripts/verify_markstein.c checks 1.6e9 pairs
-//                       over every divisor mantissa: 0 mismatches.  The
-//                       exponent ranges that theorem needs are enforced by
-//                       ray_fast_ok() per ray and by the scene check at upload;
-//                       a ray outside them takes traverse<false> (IEEE
-//                       division), so results are always the reference's.
+// Closest-hit queries come in two families:
+//   BVH traversals   the reference's own walk of its SAH tree (near child
+//                    first, far child pushed, no re-test on pop), as
+//                    traverse_reference (the straight statement, IEEE
+//                    division everywhere: MM_PIPE_REFERENCE) and the
+//                    production loop forms below.  With kFast every slab
+//                    division (bound - o) / d uses a per-ray correctly rounded
+//                    reciprocal y = RN(1/d) and Markstein's correction
+//                        q = a*y;  r = fma(-q, d, a);  q' = fma(r, y, q)
+//                    which equals RN(a/d) when no under/overflow occurs
+//                    (Markstein 1990; Cornea-Hasegan, Golliver, Markstein
+//                    1999; scripts/verify_markstein.c checks 1.6e9 pairs
+//                    over every divisor mantissa).  The exponent ranges that
+//                    theorem needs are enforced by ray_fast_ok() per ray and
+//                    by the scene check at upload; a ray outside them takes
+//                    traverse<false> (IEEE division).
+//   grid search      (mm_grid.h) a certified search that returns the same
+//                    (t, index) as the reference walk without walking it.
 #pragma once
 
 #include "mm_device.h"
@@ -121,62 +124,15 @@ __device__ __forceinline__ float aabb_pairs(float4 a, float4 b, const Ray& r, fl
 }
 
 // ---------------------------------------------------------------------------
-// Traversal stack policies.  Entries are packed child words
-// (count << 24 | left_first).  The stack never holds more entries than the
-// tree is deep (one pending far child per level of the current path).
-struct ScratchStack {          // the reference's 50-entry private array
+// The reference's 50-entry private traversal stack (scratch).  Entries are
+// packed child words (count << 24 | left_first); the stack never holds more
+// entries than the tree is deep (one pending far child per level).
+struct ScratchStack {
     uint32_t s[kStackMax];
     static constexpr uint32_t kCap = kStackMax;
     __device__ __forceinline__ void push(uint32_t i, uint32_t v) { s[i] = v; }
     __device__ __forceinline__ uint32_t pop(uint32_t i) const { return s[i]; }
 };
-// The reference stack with u16 entries (count << 12 | left_first; needs
-// count < 16 and left_first < 4096, checked at upload): half the scratch
-// footprint, so the traversal stacks of all resident waves stay in L2.
-struct ScratchStack16 {
-    uint16_t s[kStackMax];
-    static constexpr uint32_t kCap = kStackMax;
-    __device__ __forceinline__ void push(uint32_t i, uint32_t v) {
-        s[i] = (uint16_t)(((v >> 24) << 12) | (v & 0xFFFu));
-    }
-    __device__ __forceinline__ uint32_t pop(uint32_t i) const {
-        const uint32_t p = s[i];
-        return ((p >> 12) << 24) | (p & 0xFFFu);
-    }
-};
-// The same stack with its top entry held in a register: a pop returns the
-// register and reloads the next entry from scratch, whose latency then
-// overlaps the following traversal step instead of stalling the next node
-// fetch.  mem[k] holds entry k-1 (mem[0] is a dummy), so push and pop are
-// unconditional.
-struct RegTopStack {
-    uint32_t top = 0;
-    uint32_t mem[kStackMax + 1];
-    static constexpr uint32_t kCap = kStackMax;
-    __device__ __forceinline__ void push(uint32_t i, uint32_t v) { mem[i] = top; top = v; }
-    __device__ __forceinline__ uint32_t pop(uint32_t i) {
-        const uint32_t r = top;
-        top = mem[i];
-        return r;
-    }
-};
-// u16 entries in LDS, [slot][thread] so a wave's same-slot accesses are
-// contiguous: (count << 12 | left_first) needs count < 16, left_first < 4096
-// and slots >= tree depth -- all checked at upload.
-struct LdsStack16 {
-    uint16_t* base;            // &lds[slot 0][this thread]
-    uint32_t stride;           // threads per block
-    uint32_t cap;
-    __device__ __forceinline__ void push(uint32_t i, uint32_t v) {
-        base[i * stride] = (uint16_t)(((v >> 24) << 12) | (v & 0xFFFu));
-    }
-    __device__ __forceinline__ uint32_t pop(uint32_t i) const {
-        const uint32_t p = base[i * stride];
-        return ((p >> 12) << 24) | (p & 0xFFFu);
-    }
-};
-template <typename S> __device__ __forceinline__ uint32_t stack_cap(const S& st) { return st.kCap; }
-template <> __device__ __forceinline__ uint32_t stack_cap<LdsStack16>(const LdsStack16& st) { return st.cap; }
 
 // ---------------------------------------------------------------------------
 // Scene views: where a traversal reads nodes and (optionally) the compact,
@@ -211,9 +167,6 @@ struct SplitNodes {
 __device__ __forceinline__ void node_pair(const float4* n, uint32_t lf, float4& la, float4& lb, float4& ra,
                                           float4& rb) {
     la = n[2 * lf]; lb = n[2 * lf + 1]; ra = n[2 * lf + 2]; rb = n[2 * lf + 3];
-#ifdef MM_FORCE_B128
-    asm volatile("" ::"v"(lb.w), "v"(rb.w));  // experiment: 16-B reads instead of 12-B (ds_read_b96)
-#endif
 }
 __device__ __forceinline__ void node_pair(const SplitNodes& n, uint32_t lf, float4& la, float4& lb, float4& ra,
                                           float4& rb) {
@@ -309,102 +262,53 @@ __device__ __forceinline__ void leaf_tests(const DevScene& sc, const V& v, uint3
 // stack holds packed words, so a pop needs no node load.  Visit order,
 // pruning and pushes are exactly the reference's.
 //
-// trav_step runs ONE iteration of the reference's while(true) loop
-// (shaders.metal:126-155) on explicit state (cur, head, stack) and returns
-// true when the traversal is over (ovf set on stack overflow), so a caller
-// can interleave traversal steps of different rays (k_trace_persist).
-template <bool kFast, bool kStats, typename V, typename Stack>
-__device__ __forceinline__ bool trav_step(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                          uint32_t& index, uint32_t& cur, uint32_t& head, Stack& stack,
-                                          Counters& c, bool& ovf) {
-    const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
-    if (cnt > 0) {
-        leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
-        if (kStats) c.rtests += cnt;
-        if (head == 0) return true;
-        cur = stack.pop(--head);
-        return false;
-    }
-    if (kStats) c.visits++;
-    float4 la, lb, ra, rb;
-    node_pair(v.nodes, lf, la, lb, ra, rb);
-    float d1 = aabb_pairs<kFast>(la, lb, r, t);
-    float d2 = aabb_pairs<kFast>(ra, rb, r, t);
-    uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
-    if (d1 > d2) {
-        const float tt = d1; d1 = d2; d2 = tt;
-        const uint32_t x = pl; pl = pr; pr = x;
-    }
-    if (d1 == kBig) {
-        if (head == 0) return true;
-        cur = stack.pop(--head);
-    } else {
-        cur = pl;
-        if (d2 != kBig) {
-            if (head >= stack_cap(stack)) { ovf = true; return true; }
-            stack.push(head++, pr);
-        }
-    }
-    return false;
-}
-
-template <bool kFast, bool kStats, typename V, typename Stack>
-__device__ __forceinline__ bool traverse(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                         uint32_t& index, Stack& stack, Counters& c) {
-    uint32_t cur = sc.root_packed, head = 0;
-    bool ovf = false;
-    while (!trav_step<kFast, kStats>(sc, v, r, t, index, cur, head, stack, c, ovf)) {
-    }
-    return !ovf;
-}
-
-// Lean form (MM_OPT_TRAVERSAL 2): the same iteration with one pop site and no
-// overflow test.  mm_upload_scene rejects trees deeper than the stack (50
-// entries, or the LDS stack's depth-sized slots), and near-first traversal
-// holds at most one pending far child per level of the current root-to-node
-// path, so a push can never overflow.  Per lane the visits, pushes and pops
-// are exactly trav_step's.
-template <bool kFast, bool kStats, typename V, typename Stack>
-__device__ __forceinline__ bool traverse_lean(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                              uint32_t& index, Stack& stack, Counters& c) {
+// If-if loop (form 0): ONE iteration of the reference's while(true) loop
+// (shaders.metal:126-155) per loop trip.
+template <bool kFast, bool kStats, typename V>
+__device__ __forceinline__ bool traverse(const DevScene& sc, const V& v, const Ray& r, float& t, uint32_t& index,
+                                         ScratchStack& stack, Counters& c) {
     uint32_t cur = sc.root_packed, head = 0;
     for (;;) {
         const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
-        bool pop;
         if (cnt > 0) {
             leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
             if (kStats) c.rtests += cnt;
-            pop = true;
-        } else {
-            if (kStats) c.visits++;
-            float4 la, lb, ra, rb;
-            node_pair(v.nodes, lf, la, lb, ra, rb);
-            const float d1 = aabb_pairs<kFast>(la, lb, r, t);
-            const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
-            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
-            const bool sw = d1 > d2;
-            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
-            cur = sw ? pr : pl;
-            pop = dn == kBig;
-            if (!pop && df != kBig) stack.push(head++, sw ? pl : pr);
-        }
-        if (pop) {
-            if (head == 0) break;
+            if (head == 0) return true;
             cur = stack.pop(--head);
+            continue;
+        }
+        if (kStats) c.visits++;
+        float4 la, lb, ra, rb;
+        node_pair(v.nodes, lf, la, lb, ra, rb);
+        float d1 = aabb_pairs<kFast>(la, lb, r, t);
+        float d2 = aabb_pairs<kFast>(ra, rb, r, t);
+        uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
+        if (d1 > d2) {
+            const float tt = d1; d1 = d2; d2 = tt;
+            const uint32_t x = pl; pl = pr; pr = x;
+        }
+        if (d1 == kBig) {
+            if (head == 0) return true;
+            cur = stack.pop(--head);
+        } else {
+            cur = pl;
+            if (d2 != kBig) {
+                if (head >= ScratchStack::kCap) return false;
+                stack.push(head++, pr);
+            }
         }
     }
-    return true;
 }
 
-// Leaf-then-interior form (MM_OPT_TRAVERSAL 5): one iteration runs a lane's
-// leaf tests (if it sits at a leaf) and pops, and then, if the lane is now at
-// an interior node, that node's step.  Per lane the sequence of leaf tests,
-// node visits, pushes and pops is exactly trav_step's; a leaf visit just no
-// longer costs the wave an iteration of its own (wave model,
-// scripts/wave_sim.cpp: 7 % fewer iterations on C3).
-template <bool kFast, bool kStats, typename V, typename Stack>
+// Leaf-then-interior form (form 5): one iteration runs a lane's leaf tests (if
+// it sits at a leaf) and pops, and then, if the lane is now at an interior
+// node, that node's step.  Per lane the sequence of leaf tests, node visits,
+// pushes and pops is exactly the if-if loop's; a leaf visit just no longer
+// costs the wave an iteration of its own (C3 11.06 -> 10.37 ms,
+// profiles/r01_ab_leafinterior.txt).
+template <bool kFast, bool kStats, typename V>
 __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                            uint32_t& index, Stack& stack, Counters& c) {
+                                            uint32_t& index, ScratchStack& stack, Counters& c) {
     uint32_t cur = sc.root_packed, head = 0;
     for (;;) {
         if ((cur >> 24) != 0) {
@@ -430,7 +334,7 @@ __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, cons
             } else {
                 cur = sw ? pr : pl;
                 if (df != kBig) {
-                    if (head >= stack_cap(stack)) return false;
+                    if (head >= ScratchStack::kCap) return false;
                     stack.push(head++, sw ? pl : pr);
                 }
             }
@@ -439,14 +343,15 @@ __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, cons
     return true;
 }
 
-// Lean leaf-then-interior form (MM_OPT_TRAVERSAL 7) for scenes without SLOW
-// rect records (mm_upload_scene sets lean_ok): the leaf test is
-// rect_test_compact_lean (no kind branches) and pushes skip the overflow test (upload rejects trees
+// Lean leaf-then-interior form (form 7) for scenes without SLOW rect records
+// (mm_upload_scene sets lean_ok): the leaf test is rect_test_compact_lean (no
+// kind branches) and pushes skip the overflow test (upload rejects trees
 // deeper than the stack; near-first traversal holds at most one pending far
-// child per level).  Per lane the operation sequence is traverse_li's.
-template <bool kStats, typename V, typename Stack>
+// child per level).  Per lane the operation sequence is traverse_li's
+// (C3 10.40 -> 9.53 ms, profiles/r01_ab_lean.txt).
+template <bool kStats, typename V>
 __device__ __forceinline__ bool traverse_lil(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                             uint32_t& index, Stack& stack, Counters& c) {
+                                             uint32_t& index, ScratchStack& stack, Counters& c) {
     uint32_t cur = sc.root_packed, head = 0;
     for (;;) {
         if ((cur >> 24) != 0) {
@@ -478,238 +383,11 @@ __device__ __forceinline__ bool traverse_lil(const DevScene& sc, const V& v, con
     return true;
 }
 
-// ---------------------------------------------------------------------------
-// Verified conservative closest hit (MM_OPT_TRAVERSAL 9).
-//
-// Search: the same BVH with every box expanded by an absolute margin E
-// (mm_upload_scene) and slab quotients RN(RN(b - o) * RN(1/d)) -- two
-// operations instead of the exact quotient's four -- culling only boxes whose
-// approximate interval starts beyond the best hit so far (<=, so ties
-// survive).  Every rect reached gets the exact reference test (the compact
-// record's operations) without its `a < t` clause; the minimum a* and its slot
-// are kept with a tie flag.
-//
-// Why the search cannot miss the reference's answer: a rect the reference
-// accepts at a has o + a*d within delta <= ~10u*C of the rect per axis
-// (u = 2^-24, C >= every |coordinate| and |origin component|), so inside its
-// leaf box, and every ancestor box, expanded by E, with margin E - delta; an
-// approximate quotient is within 3u*|b - o|/|d| <= 6u*C/|d| of the exact one,
-// so with E >= 64*(10u + 6u)*C the approximate interval of every expanded
-// ancestor contains a.  Hence a* is the minimum over ALL rects the reference
-// would accept at any t, and a tie flag is exact.
-//
-// Verification (exactness of the answer, not of the search): with a* unique,
-// the reference's current best is > a* whenever it tests a box on R*'s path,
-// and the exact (reference-arithmetic) slab values of every ancestor box
-// bracket those of R*'s leaf box (RN and Markstein division are monotone,
-// ancestors contain the leaf).  So if the leaf box's exact test gives
-// tmax >= tmin, tmax > 0 and tmin <= a*, the reference reaches R*, accepts it,
-// and never replaces it: its answer is (a*, R*).  A tie, a failed check, or a
-// ray outside the guards runs traverse_li on the exact nodes instead.
-// scripts/cons_sim.cpp replays C3 / C5 / P0 frames on the CPU: 0 mismatches
-// in 37 M queries, ties only where coplanar rects overlap (P0's outer walls).
-
-// RN(RN(b - o) * y): the approximate slab quotient
-__device__ __forceinline__ float qapprox(float b, float o, float y) { return (b - o) * y; }
-
-__device__ __forceinline__ float aabb_cons(float4 a, float4 b, const Ray& r, float best) {
-    const float tx1 = qapprox(a.x, r.o.x, r.y.x), tx2 = qapprox(a.y, r.o.x, r.y.x);
-    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
-    const float ty1 = qapprox(a.z, r.o.y, r.y.y), ty2 = qapprox(a.w, r.o.y, r.y.y);
-    tmin = fmaxf(tmin, fminf(ty1, ty2));
-    tmax = fminf(tmax, fmaxf(ty1, ty2));
-    const float tz1 = qapprox(b.x, r.o.z, r.y.z), tz2 = qapprox(b.y, r.o.z, r.y.z);
-    tmin = fmaxf(tmin, fminf(tz1, tz2));
-    tmax = fminf(tmax, fmaxf(tz1, tz2));
-    return (tmax >= tmin && tmin <= best && tmax > 0.0f) ? tmin : kBig;
-}
-
-// Exact compact rect test (FAST / SKIP records) without the `a < t` clause:
-// a if the reference would accept the rect at a large enough t, else kBig.
-template <typename R>
-__device__ __forceinline__ float rect_a_compact(const R& recs, uint32_t slot, const Ray& r) {
-    const uint2 w01 = recs[5 * slot + 0], w23 = recs[5 * slot + 1], w45 = recs[5 * slot + 2],
-                w67 = recs[5 * slot + 3], w89 = recs[5 * slot + 4];
-    const uint32_t meta = w89.y;
-    const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
-    const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
-    const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
-    const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
-    const bool hit = x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) &&
-                     x2 >= __uint_as_float(w67.y) && x2 <= __uint_as_float(w89.x) && a > 0.1f;
-    return hit ? a : kBig;
-}
-
-__device__ __forceinline__ bool cons_ray_ok(const DevScene& sc, const Ray& r) {
-    return fabsf(r.o.x) <= sc.cons_bound && fabsf(r.o.y) <= sc.cons_bound && fabsf(r.o.z) <= sc.cons_bound;
-}
-
-template <bool kStats, typename V, typename Stack>
-__device__ __forceinline__ bool traverse_cons(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                              uint32_t& index, Stack& stack, Counters& c) {
-    uint32_t cur = sc.root_packed, head = 0, bslot = 0;
-    float best = kBig;
-    bool tie = false;
-    for (;;) {
-        if ((cur >> 24) != 0) {
-            const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
-            for (uint32_t i = 0; i < cnt; ++i) {
-                const float a = rect_a_compact(v.recs, lf + i, r);
-                tie = tie || (a == best && a != kBig);
-                if (a < best) {
-                    best = a;
-                    bslot = lf + i;
-                    tie = false;
-                }
-            }
-            if (kStats) c.rtests += cnt;
-            if (head == 0) break;
-            cur = stack.pop(--head);
-        }
-        if ((cur >> 24) == 0) {
-            const uint32_t lf = cur & 0xFFFFFFu;
-            if (kStats) c.visits++;
-            float4 la, lb, ra, rb;
-            node_pair(v.nodes, lf, la, lb, ra, rb);
-            const float d1 = aabb_cons(la, lb, r, best);
-            const float d2 = aabb_cons(ra, rb, r, best);
-            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
-            const bool sw = d1 > d2;
-            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
-            if (dn == kBig) {
-                if (head == 0) break;
-                cur = stack.pop(--head);
-            } else {
-                cur = sw ? pr : pl;
-                if (df != kBig) stack.push(head++, sw ? pl : pr);
-            }
-        }
-    }
-    if (best == kBig) return true;  // no rect hit: (kBig, index untouched)
-    if (!tie) {
-        const float4 a = sc.slot_box[2 * bslot], b = sc.slot_box[2 * bslot + 1];
-        const float tx1 = qdiv(a.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(a.y - r.o.x, r.d.x, r.y.x);
-        float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
-        const float ty1 = qdiv(a.z - r.o.y, r.d.y, r.y.y), ty2 = qdiv(a.w - r.o.y, r.d.y, r.y.y);
-        tmin = fmaxf(tmin, fminf(ty1, ty2));
-        tmax = fminf(tmax, fmaxf(ty1, ty2));
-        const float tz1 = qdiv(b.x - r.o.z, r.d.z, r.y.z), tz2 = qdiv(b.y - r.o.z, r.d.z, r.y.z);
-        tmin = fmaxf(tmin, fminf(tz1, tz2));
-        tmax = fminf(tmax, fmaxf(tz1, tz2));
-        if (tmax >= tmin && tmax > 0.0f && tmin <= best) {
-            t = best;
-            index = v.recs[5 * bslot + 4].y & 0xFFFFFu;
-            return true;
-        }
-    }
-    // tie or unverified: the reference query on the exact nodes (global memory)
-    return traverse_li<true, false>(sc, view(sc.nodes_exact, v.recs), r, t, index, stack, c);
-}
-
-// "while-while" form of the same traversal: each lane runs interior steps
-// until it reaches a leaf (or finishes), then the wave's leaves are processed
-// together.  Per lane the sequence of node visits, rect tests, pushes and
-// pops is exactly trav_step's (no speculation: a leaf is always tested
-// before the next node is visited), so results are identical; only the
-// interleaving of lanes' work inside a wave changes.
-template <bool kFast, bool kStats, typename V, typename Stack>
-__device__ __forceinline__ bool traverse_ww(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                            uint32_t& index, Stack& stack, Counters& c) {
-    uint32_t cur = sc.root_packed, head = 0;
-    for (;;) {
-        // interior phase
-        bool done = false;
-        while ((cur >> 24) == 0) {
-            const uint32_t lf = cur & 0xFFFFFFu;
-            if (kStats) c.visits++;
-            float4 la, lb, ra, rb;
-            node_pair(v.nodes, lf, la, lb, ra, rb);
-            const float d1 = aabb_pairs<kFast>(la, lb, r, t);
-            const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
-            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
-            const bool sw = d1 > d2;
-            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
-            const uint32_t pn = sw ? pr : pl, pf = sw ? pl : pr;
-            if (dn == kBig) {
-                if (head == 0) { done = true; break; }
-                cur = stack.pop(--head);
-            } else {
-                cur = pn;
-                if (df != kBig) {
-                    if (head >= stack_cap(stack)) return false;
-                    stack.push(head++, pf);
-                }
-            }
-        }
-        if (done) break;
-        // leaf phase
-        const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
-        leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
-        if (kStats) c.rtests += cnt;
-        if (head == 0) break;
-        cur = stack.pop(--head);
-    }
-    return true;
-}
-
-// Leaf-batched form: every iteration the wave runs EITHER one interior step
-// for the lanes inside the tree OR the leaf tests for the lanes waiting at a
-// leaf -- the latter once at least `kBatch` lanes wait (or every unfinished
-// lane does).  A lane at a leaf does nothing until its leaf is tested, so per
-// lane the operation sequence is exactly trav_step's; only the interleaving
-// between lanes changes.  Avoids paying the leaf body (rect records, ~40 VALU)
-// in nearly every iteration as the if-if loop does (P(some lane of 64 at a
-// leaf) ~ 99 % at 1.47 leaf visits per 18.3 interior visits).
-template <bool kFast, bool kStats, uint32_t kBatch, typename V, typename Stack>
-__device__ __forceinline__ bool traverse_lb(const DevScene& sc, const V& v, const Ray& r, float& t,
-                                            uint32_t& index, Stack& stack, Counters& c) {
-    uint32_t cur = sc.root_packed, head = 0;
-    bool done = false, ovf = false;
-    for (;;) {
-        const bool at_leaf = !done && (cur >> 24) != 0;
-        const uint64_t live = __ballot(!done);
-        if (live == 0) break;
-        const uint64_t leaves = __ballot(at_leaf);
-        const bool do_leaves = leaves != 0 && (leaves == live || (uint32_t)__popcll(leaves) >= kBatch);
-        if (do_leaves) {
-            if (at_leaf) {
-                const uint32_t lf = cur & 0xFFFFFFu, cnt = cur >> 24;
-                leaf_tests<kFast>(sc, v, lf, cnt, r, t, index);
-                if (kStats) c.rtests += cnt;
-                if (head == 0) done = true;
-                else cur = stack.pop(--head);
-            }
-        } else if (!done && !at_leaf) {
-            const uint32_t lf = cur & 0xFFFFFFu;
-            if (kStats) c.visits++;
-            float4 la, lb, ra, rb;
-            node_pair(v.nodes, lf, la, lb, ra, rb);
-            const float d1 = aabb_pairs<kFast>(la, lb, r, t);
-            const float d2 = aabb_pairs<kFast>(ra, rb, r, t);
-            const uint32_t pl = __float_as_uint(lb.z), pr = __float_as_uint(rb.z);
-            const bool sw = d1 > d2;
-            const float dn = sw ? d2 : d1, df = sw ? d1 : d2;
-            const uint32_t pn = sw ? pr : pl, pf = sw ? pl : pr;
-            if (dn == kBig) {
-                if (head == 0) done = true;
-                else cur = stack.pop(--head);
-            } else {
-                cur = pn;
-                if (df != kBig) {
-                    if (head >= stack_cap(stack)) { ovf = true; done = true; }
-                    else stack.push(head++, pf);
-                }
-            }
-        }
-    }
-    return !ovf;
-}
-
 // The straight statement of intersect_bvh_iterative over the reference node
 // layout (sc.nodes_ref, 2 float4 per node: a, (mx.yz, lf, count)).
-template <bool kStats, typename Stack>
+template <bool kStats>
 __device__ __forceinline__ bool traverse_reference(const DevScene& sc, const Ray& r, float& t, uint32_t& index,
-                                                   Stack& stack, Counters& c) {
+                                                   ScratchStack& stack, Counters& c) {
     const float4* __restrict__ nodes = sc.nodes_ref;
     uint32_t node = 0, head = 0;
     for (;;) {
@@ -744,33 +422,20 @@ __device__ __forceinline__ bool traverse_reference(const DevScene& sc, const Ray
     return true;
 }
 
-// Closest hit for one ray: production traversal with the exact fallback.
-// kWW selects the while-while loop structure.
-template <bool kStats, typename V, typename Stack, int kWW = 0>
-__device__ __forceinline__ bool closest_hit(const DevScene& sc, const V& v, F3 o, F3 d, float& t,
-                                            uint32_t& index, Stack& stack, Counters& c) {
-    const Ray r = make_ray(o, d);
-    if constexpr (kWW == 2) {
-        if (sc.fast_ok && ray_fast_ok(r)) return traverse_lean<true, kStats>(sc, v, r, t, index, stack, c);
-        return traverse_lean<false, kStats>(sc, v, r, t, index, stack, c);
-    } else if constexpr (kWW >= 8 && kWW != 9) {
-        if (sc.fast_ok && ray_fast_ok(r)) return traverse_lb<true, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
-        return traverse_lb<false, kStats, (uint32_t)kWW>(sc, v, r, t, index, stack, c);
-    } else if constexpr (kWW == 9) {
-        if (sc.fast_ok && ray_fast_ok(r) && cons_ray_ok(sc, r))
-            return traverse_cons<kStats>(sc, v, r, t, index, stack, c);
-        return traverse_li<false, kStats>(sc, view(sc.nodes_exact, v.recs), r, t, index, stack, c);
-    } else if constexpr (kWW == 7) {
-        if (sc.fast_ok && ray_fast_ok(r)) return traverse_lil<kStats>(sc, v, r, t, index, stack, c);
+// Closest hit for one ray by the BVH: production traversal with the exact
+// (IEEE-division) fallback for rays outside the Markstein guards.
+template <bool kStats, int kForm, typename V>
+__device__ __forceinline__ bool closest_hit_bvh(const DevScene& sc, const V& v, const Ray& r, float& t,
+                                                uint32_t& index, ScratchStack& stack, Counters& c) {
+    const bool fast = sc.fast_ok && ray_fast_ok(r);
+    if constexpr (kForm == kFormLean) {
+        if (fast) return traverse_lil<kStats>(sc, v, r, t, index, stack, c);
         return traverse_li<false, kStats>(sc, v, r, t, index, stack, c);
-    } else if constexpr (kWW == 5) {
-        if (sc.fast_ok && ray_fast_ok(r)) return traverse_li<true, kStats>(sc, v, r, t, index, stack, c);
+    } else if constexpr (kForm == kFormLeafInterior) {
+        if (fast) return traverse_li<true, kStats>(sc, v, r, t, index, stack, c);
         return traverse_li<false, kStats>(sc, v, r, t, index, stack, c);
-    } else if constexpr (kWW == 1) {
-        if (sc.fast_ok && ray_fast_ok(r)) return traverse_ww<true, kStats>(sc, v, r, t, index, stack, c);
-        return traverse_ww<false, kStats>(sc, v, r, t, index, stack, c);
     } else {
-        if (sc.fast_ok && ray_fast_ok(r)) return traverse<true, kStats>(sc, v, r, t, index, stack, c);
+        if (fast) return traverse<true, kStats>(sc, v, r, t, index, stack, c);
         return traverse<false, kStats>(sc, v, r, t, index, stack, c);
     }
 }
@@ -821,52 +486,6 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         p.mh += 1;
     }
     return true;
-}
-
-// Where a path's throughput T and radiance L live while its ray traverses
-// (they are only touched by shading): in registers (NoCold), or parked in LDS,
-// [field][thread], which frees six VGPRs for the traversal loop.
-struct NoCold {
-    __device__ __forceinline__ void save(const F3&, const F3&) const {}
-    __device__ __forceinline__ void restore(F3&, F3&) const {}
-};
-struct LdsCold {
-    float* base;        // &lds[field 0][this thread]
-    uint32_t stride;    // threads per block
-    __device__ __forceinline__ void save(const F3& T, const F3& L) const {
-        base[0] = T.x; base[stride] = T.y; base[2 * stride] = T.z;
-        base[3 * stride] = L.x; base[4 * stride] = L.y; base[5 * stride] = L.z;
-    }
-    __device__ __forceinline__ void restore(F3& T, F3& L) const {
-        T = F3{base[0], base[stride], base[2 * stride]};
-        L = F3{base[3 * stride], base[4 * stride], base[5 * stride]};
-    }
-};
-
-// Whole path (shaders.metal:302-344): returns sqrt(max(L, 0)).
-// kRef selects traverse_reference (MM_PIPE_REFERENCE).
-template <bool kStats, bool kRef, typename V, typename Stack, int kWW = 0, typename Cold = NoCold>
-__device__ __forceinline__ F3 trace_path(const DevScene& sc, const V& v, F3 ori, F3 dir, uint32_t seed,
-                                         int bounce_limit, int mirror_limit, Stack& stack, Counters& c,
-                                         bool& overflow, const Cold& cold = Cold{}) {
-    PathState p;
-    p.ori = ori; p.dir = dir; p.seed = seed;
-    p.T = F3{1.0f, 1.0f, 1.0f};
-    p.L = F3{0.0f, 0.0f, 0.0f};
-    p.mh = 0;
-    for (p.n = 0; p.n < bounce_limit + p.mh; ++p.n) {
-        float t = kBig;
-        uint32_t k = 0;
-        bool ok;
-        cold.save(p.T, p.L);
-        if constexpr (kRef) ok = traverse_reference<kStats>(sc, make_ray(p.ori, p.dir), t, k, stack, c);
-        else ok = closest_hit<kStats, V, Stack, kWW>(sc, v, p.ori, p.dir, t, k, stack, c);
-        cold.restore(p.T, p.L);
-        if (kStats) c.rays++;
-        if (!ok) { overflow = true; break; }
-        if (!shade_step(sc, p, t, k, mirror_limit)) break;
-    }
-    return F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))};
 }
 
 }  // namespace mm

@@ -1,15 +1,17 @@
 // trace_kernels.hip — gfx950 kernels for mirror-maze's per-pixel ray-trace loop.
 //
-//   k_prep_rects      per-rect subexpressions of ray_rect_intersect
-//   k_trace_chunks    parity mode: the reference dispatch (shaders.metal:245-368)
-//   k_trace_mega      throughput mode, one thread per (pixel, sample) path
-//   k_resolve         per-pixel sample reduction in the reference's order
+//   k_prep_rects         per-rect subexpressions of ray_rect_intersect
+//   k_trace_chunks       parity mode: the reference dispatch (shaders.metal:245-368)
+//   k_trace_mega         throughput mode, one thread per (pixel, sample) path
+//                        (and MM_PIPE_REFERENCE, the straight statement)
+//   k_trace_wavepersist  throughput mode, the production kernel: resident
+//                        blocks, waves pull 64-path chunks, pixels resolved in
+//                        the wave
+//   k_resolve            per-pixel sample reduction in the reference's order
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "mm_launch.h"
-#include "mm_trace.h"
+#include "mm_path.h"
 #include "mm_wave_util.h"
 
 namespace mm {
@@ -31,8 +33,8 @@ __global__ void k_prep_rects(const mm_rect* __restrict__ rects, uint32_t n, floa
     geo[4 * k + 3] = make_float4(u.x, u.y, u.z, 1.0f / lu);
 }
 
-hipError_t launch_prep_rects(const mm_rect* rects_dev, uint32_t n, float4* geo_dev, hipStream_t s) {
-    hipLaunchKernelGGL(k_prep_rects, dim3((n + 255) / 256), dim3(256), 0, s, rects_dev, n, geo_dev);
+hipError_t launch_prep_rects(const mm_rect* rects, uint32_t n, float4* geo_dev, hipStream_t s) {
+    hipLaunchKernelGGL(k_prep_rects, dim3((n + 255) / 256), dim3(256), 0, s, rects, n, geo_dev);
     return hipGetLastError();
 }
 
@@ -63,7 +65,8 @@ __global__ __launch_bounds__(1024) void k_trace_chunks(DevScene sc, mm_uniform u
     ScratchStack stack;
     Counters c;
     bool overflow = false;
-    F3 s = trace_path<kStats, false>(sc, view(sc.nodes), ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
+    const BvhQuery<kStats, kFormIfIf, NodeView<const float4*>> q{sc, view(sc.nodes)};
+    F3 s = trace_path<kStats>(sc, q, ori, d, seed, 5, 15, stack, c, overflow);  // shaders.metal:294-295
     if (overflow) atomicOr(err, 1u);
     // level 1..3: test[f] += test[f+1], += test[f+2], += test[f+4]
     s = s + F3{__shfl_xor(s.x, 1), __shfl_xor(s.y, 1), __shfl_xor(s.z, 1)};
@@ -95,17 +98,12 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
 }
 
 // ---------------------------------------------------------------------------
-// Throughput mode megakernel: path = pixel*spp + sample.
+// Throughput mode, one thread per path: path = pixel*spp + sample.
 //   kRef  : traverse_reference (IEEE division everywhere), for A/B
 //   kLds  : stage the node array in LDS (dynamic shared memory) first
-template <bool kStats, bool kRef, bool kLds>
-__global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
-                                                     unsigned long long* stats, uint32_t* err) {
-    extern __shared__ float4 lds_nodes[];
-    if constexpr (kLds) {
-        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
-        __syncthreads();
-    }
+template <bool kStats, typename Q>
+__device__ __forceinline__ void mega_body(const DevScene& sc, const Q& q, const TileJob& job,
+                                          float4* __restrict__ samples, unsigned long long* stats, uint32_t* err) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;
     const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
@@ -119,28 +117,43 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
         const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
         ScratchStack stack;
         bool overflow = false;
-        F3 s;
-        if constexpr (kLds)
-            s = trace_path<kStats, kRef>(sc, view(lds_nodes), ori, d, seed, (int)job.e.bounce_limit,
-                                         (int)job.e.mirror_limit, stack, c, overflow);
-        else
-            s = trace_path<kStats, kRef>(sc, view(sc.nodes), ori, d, seed, (int)job.e.bounce_limit,
-                                         (int)job.e.mirror_limit, stack, c, overflow);
+        const F3 s = trace_path<kStats>(sc, q, ori, d, seed, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack,
+                                        c, overflow);
         if (overflow) atomicOr(err, 1u);
         samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
     }
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
 }
 
-// Wave-persistent megakernel: resident blocks (LDS filled once per block);
-// each wave takes 64 consecutive paths at a time from a global counter and
-// traces them exactly like k_trace_mega, so no block waits for its slowest
-// wave before the CU can take more work.
-template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
-__device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V& v, Stack& stack,
-                                                 const TileJob& job, float4* __restrict__ samples,
-                                                 unsigned long long* stats, uint32_t* err, uint32_t* work,
-                                                 const Cold& cold = Cold{}) {
+template <bool kStats, bool kRef, bool kLds>
+__global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                     unsigned long long* stats, uint32_t* err) {
+    if constexpr (kRef) {
+        mega_body<kStats>(sc, RefQuery<kStats>{sc}, job, samples, stats, err);
+    } else if constexpr (kLds) {
+        extern __shared__ float4 lds_nodes[];
+        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
+        __syncthreads();
+        mega_body<kStats>(sc, BvhQuery<kStats, kFormIfIf, NodeView<float4*>>{sc, view(lds_nodes)}, job, samples,
+                          stats, err);
+    } else {
+        mega_body<kStats>(sc, BvhQuery<kStats, kFormIfIf, NodeView<const float4*>>{sc, view(sc.nodes)}, job,
+                          samples, stats, err);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-persistent megakernel: resident 1024-thread blocks (two per CU at
+// <= 64 VGPRs, 8 waves per SIMD) fill LDS once; each wave takes 64
+// consecutive paths at a time from a global counter and traces them, so no
+// block waits for its slowest wave before the CU can take more work.  With
+// 64 % spp == 0 the wave's 64 paths are whole pixels and it resolves them
+// itself (job.fuse).  A multi-frame launch queues frame 0's chunks, then frame
+// 1's, ...; a chunk's frame picks its RNG frame and output slice.
+template <bool kStats, typename Q>
+__device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
+                                                     float4* __restrict__ samples, unsigned long long* stats,
+                                                     uint32_t* err, uint32_t* work) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;         // per frame
     const uint32_t cpf = (n_paths + 63u) / 64u;           // 64-path chunks per frame
@@ -148,41 +161,17 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
     const uint32_t lane = threadIdx.x & 63u;
     const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
     Counters c;
+    ScratchStack stack;
     uint32_t paths = 0, chunks = 0;
-    const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
-    const uint32_t grab = 64u * job.grab;   // paths claimed per atomic (MM_OPT_GRAB chunks)
-    uint32_t next = 0, end = 0;             // wave-uniform claimed range
     for (;;) {
-        if (next >= end) {
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(work, grab);
-            next = __builtin_amdgcn_readfirstlane(b);
-            end = min(next + grab, n_queue);
-        }
-        const uint32_t base = next;
-        next += 64u;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(work, 64u);
+        const uint32_t base = __builtin_amdgcn_readfirstlane(b);
         if (base >= n_queue) break;
-        // MM_OPT_FAIR: a wave behind the mean chunk count runs at raised issue
-        // priority (the SIMD arbiter otherwise favours the oldest waves: chunk
-        // counts per wave spread 9-59 on C3, 28-37 with this on; the frame time
-        // does not change -- profiles/r01_timeline_probe.txt).
-        if (job.fair) {
-            if (__builtin_amdgcn_readfirstlane((uint64_t)chunks * n_waves < base / 64u ? 1u : 0u))
-                __builtin_amdgcn_s_setprio(1);
-            else
-                __builtin_amdgcn_s_setprio(0);
-        }
         ++chunks;
-        // MM_OPT_CHUNK_ORDER: queue position -> chunk through the cost-sorted
-        // permutation (paths are keyed by pixel/sample, so any order gives the
-        // same samples); the chunk's duration is recorded for the next sort
-        // queue position -> (frame, chunk of the frame); one frame: frame 0, chunk = position
-        const uint32_t q = base >> 6;
-        const uint32_t fr = job.n_frames > 1 ? q / cpf : 0u;
-        const uint32_t qc = q - fr * cpf;
-        const uint32_t chunk = job.order ? __builtin_amdgcn_readfirstlane(job.order[qc]) : qc;
-        const unsigned long long t_chunk = job.cost ? (unsigned long long)wall_clock64() : 0ull;
-        const uint32_t path = chunk * 64u + lane;
+        const uint32_t qc = base >> 6;
+        const uint32_t fr = job.n_frames > 1 ? qc / cpf : 0u;
+        const uint32_t path = (qc - fr * cpf) * 64u + lane;
         const bool valid = path < n_paths;
         F3 s = F3{0.0f, 0.0f, 0.0f};
         if (valid) {
@@ -192,128 +181,29 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const V
             uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame + fr);
             const F3 d = jitter(primary_dir(job.u, px, py), seed);
             bool overflow = false;
-            s = trace_path<kStats, false, V, Stack, kWW>(sc, v, ori, d, seed, (int)job.e.bounce_limit,
-                                                         (int)job.e.mirror_limit, stack, c, overflow, cold);
+            s = trace_path<kStats>(sc, q, ori, d, seed, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c,
+                                   overflow);
             if (overflow) atomicOr(err, 1u);
             if (!job.fuse) samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
         }
         if (job.fuse) resolve_in_wave(job, s, path, valid, job.out + (size_t)fr * job.w * job.h);
-        if (job.cost && lane == 0 && fr == 0)
-            job.cost[chunk] = (uint32_t)((unsigned long long)wall_clock64() - t_chunk);
     }
     if (kStats) flush_stats(stats, c, paths);
     return chunks;
 }
 
-// Bounce-refill form of the wave-persistent body (loop form 4): a lane whose
-// path ends takes the next path of the wave's chunk at the next bounce
-// boundary instead of idling until the wave's longest path ends.  The wave
-// runs one bounce (closest hit + shade) per iteration for all lanes; every
-// path's operation sequence is trace_path's, so samples are bit-identical.
-template <bool kStats, typename V, typename Stack, int kTrav = 0, typename Cold = NoCold>
-__device__ __forceinline__ uint32_t bouncerefill_body(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
-                                                  float4* __restrict__ samples, unsigned long long* stats,
-                                                  uint32_t* err, uint32_t* work) {
-    const uint32_t spp = job.e.spp;
-    const uint32_t n_paths = job.w * job.h * spp;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const int bounce_limit = (int)job.e.bounce_limit, mirror_limit = (int)job.e.mirror_limit;
-    Counters c;
-    uint32_t paths = 0;
-    uint32_t chunk_base = 0, chunk_end = 0;  // wave-uniform
-    bool more = true, active = false;
-    uint32_t pid = 0;
-    PathState p;
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        if (idle && (more || chunk_base < chunk_end)) {
-            const uint32_t need = (uint32_t)__popcll(idle), rank = (uint32_t)__popcll(idle & lt);
-            const uint32_t take1 = min(need, chunk_end - chunk_base);
-            bool got = !active && rank < take1;
-            uint32_t mine = chunk_base + rank;
-            chunk_base += take1;
-            if (take1 < need && more) {
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(work, 64u);
-                b = __shfl(b, 0);
-                if (b >= n_paths) {
-                    more = false;
-                } else {
-                    chunk_base = b;
-                    chunk_end = min(b + 64u, n_paths);
-                    const uint32_t take2 = min(need - take1, chunk_end - chunk_base);
-                    if (!active && rank >= take1 && rank < take1 + take2) {
-                        got = true;
-                        mine = chunk_base + (rank - take1);
-                    }
-                    chunk_base += take2;
-                }
-            }
-            if (got) {
-                pid = mine;
-                const uint32_t pix = mine / spp, smp = mine - pix * spp;
-                const uint32_t j = pix / job.w, i = pix - j * job.w;
-                const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
-                p.seed = seed_tile(py * job.view_w + px, smp, job.e.frame);
-                p.dir = jitter(primary_dir(job.u, px, py), p.seed);
-                p.ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
-                p.T = F3{1.0f, 1.0f, 1.0f};
-                p.L = F3{0.0f, 0.0f, 0.0f};
-                p.n = 0;
-                p.mh = 0;
-                active = true;
-            }
-        }
-        if (!__ballot(active)) break;
-        if (active) {
-            bool fin = !(p.n < bounce_limit + p.mh);
-            if (!fin) {  // one bounce: shaders.metal:306-340
-                float t = kBig;
-                uint32_t k = 0;
-                const bool ok = closest_hit<kStats, V, Stack, kTrav>(sc, v, p.ori, p.dir, t, k, stack, c);
-                if (kStats) c.rays++;
-                if (!ok) atomicOr(err, 1u);
-                fin = !ok || !shade_step(sc, p, t, k, mirror_limit);
-                p.n++;
-                fin = fin || !(p.n < bounce_limit + p.mh);
-            }
-            if (fin) {
-                samples[pid] = make_float4(sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)),
-                                           sqrtf(fmaxf(p.L.z, 0.0f)), 0.0f);
-                paths++;
-                active = false;
-            }
-        }
-    }
-    if (kStats) flush_stats(stats, c, paths);
-    return 0;
-}
-
-template <bool kStats, int kWW, typename V, typename Stack, typename Cold = NoCold>
-__device__ __forceinline__ uint32_t wp_dispatch(const DevScene& sc, const V& v, Stack& stack, const TileJob& job,
-                                                float4* __restrict__ samples, unsigned long long* stats,
-                                                uint32_t* err, uint32_t* work, const Cold& cold = Cold{}) {
-    if constexpr (kWW == 4) return bouncerefill_body<kStats>(sc, v, stack, job, samples, stats, err, work);
-    else if constexpr (kWW == 6) return bouncerefill_body<kStats, V, Stack, 5>(sc, v, stack, job, samples, stats, err, work);
-    else return wavepersist_body<kStats, kWW>(sc, v, stack, job, samples, stats, err, work, cold);
-}
-
-// Traversal stack of the wave-persistent kernel: loop form 3 is the if-if loop
-// with the register-top stack (RegTopStack), every other form the scratch array.
-template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, ScratchStack>;
-
-// kLds: 0 nodes via L1/L2 + scratch stack, 1 nodes in LDS + scratch stack,
-// 2 nodes in LDS + u16 stack in LDS (stack_slots entries per thread),
-// 3 nodes + compact rect records in LDS, 4 top of the tree in LDS (the first
-// sc.n_lds_f4 float4s of the breadth-first node array), the rest via L1/L2,
-// 5 nodes in LDS + each path's T and L parked in LDS while it traverses,
-// 6 = 4 + compact rect records read through L1/L2, 7 = 1 + the same,
-// 8 = 2 + the same (nodes and u16 stack in LDS, rect records via L1/L2),
-// 9 = 3 with u16 traversal-stack entries in scratch, 10 dictionary-coded nodes
-// in LDS (DictNodes) + compact rect records read through L1/L2.
-// Diagnostics: time at which the block's LDS staging completed (wave timeline).
+// LDS modes (what a resident block stages before tracing; the rest is read
+// through L1/L2):
+//   0  nothing (nodes, records global)           BVH forms 0 / 5
+//   1  BVH nodes                                  BVH forms 0 / 5 (general rect test)
+//   3  BVH nodes + compact slot records           BVH forms 0 / 5 / 7
+//   6  top of the breadth-first node array        BVH forms 5 / 7 (split cache)
+//   7  BVH nodes, compact records global          BVH forms 5 / 7
+//   10 dictionary-coded nodes, records global     BVH forms 5 / 7
+//   11 the whole grid image                       grid search
+//   12 grid cells + lists, records + boxes global grid search
+//   13 nothing (the grid image global)             grid search
 #define MM_TS_STAGED()                                                                                      \
     do {                                                                                                     \
         if (job.wave_ts && (threadIdx.x & 63u) == 0) {                                                       \
@@ -322,76 +212,77 @@ template <int kWW> using WpStack = std::conditional_t<kWW == 3, RegTopStack, Scr
         }                                                                                                    \
     } while (0)
 
-template <bool kStats, int kLds, int kBlock, int kMinWaves, int kWW>
-__global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScene sc, TileJob job,
-                                                                         float4* __restrict__ samples,
-                                                                         unsigned long long* stats, uint32_t* err,
-                                                                         uint32_t* work, uint32_t stack_slots) {
+template <bool kStats, int kLds, int kForm>
+__global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                               unsigned long long* stats, uint32_t* err,
+                                                               uint32_t* work) {
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
     uint32_t chunks = 0;
-    if constexpr (kLds == 4 || kLds == 6) {
-        extern __shared__ float4 lds_top[];
-        for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds_top[i] = sc.nodes[i];
+    extern __shared__ float4 lds[];
+    if constexpr (kLds == 11 || kLds == 12) {
+        const uint32_t n16 = (kLds == 11 ? sc.grid.bytes : sc.grid.off_recs) / 16u;
+        uint4* img = reinterpret_cast<uint4*>(lds);
+        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) img[i] = sc.grid.image[i];
         __syncthreads();
         MM_TS_STAGED();
-        WpStack<kWW> st;
-        const SplitNodes nodes{lds_top, sc.nodes, sc.n_lds_f4};
-        if constexpr (kLds == 6)
-            chunks = wp_dispatch<kStats, kWW>(sc, view(nodes, sc.recs), st, job, samples, stats, err, work);
-        else
-            chunks = wp_dispatch<kStats, kWW>(sc, view(nodes), st, job, samples, stats, err, work);
-    } else if constexpr (kLds == 10) {  // dictionary-coded nodes in LDS, compact rect records via L1/L2
-        extern __shared__ float4 lds_dict[];
-        float* tab = reinterpret_cast<float*>(lds_dict);
+        const char* base = reinterpret_cast<const char*>(lds);
+        const uint32_t* cells = reinterpret_cast<const uint32_t*>(base);
+        const uint16_t* list = reinterpret_cast<const uint16_t*>(base + sc.grid.off_list);
+        if constexpr (kLds == 11) {
+            const auto gv = grid_view(cells, list, reinterpret_cast<const uint2*>(base + sc.grid.off_recs),
+                                      reinterpret_cast<const float2*>(base + sc.grid.off_box));
+            chunks = wavepersist_body<kStats>(sc, GridQuery<kStats, decltype(gv)>{sc, gv}, job, samples, stats, err,
+                                              work);
+        } else {
+            const auto gv = grid_view(cells, list, sc.grid.recs, sc.grid.box);
+            chunks = wavepersist_body<kStats>(sc, GridQuery<kStats, decltype(gv)>{sc, gv}, job, samples, stats, err,
+                                              work);
+        }
+    } else if constexpr (kLds == 13) {
+        const auto gv = grid_view(sc.grid.cells, sc.grid.list, sc.grid.recs, sc.grid.box);
+        chunks = wavepersist_body<kStats>(sc, GridQuery<kStats, decltype(gv)>{sc, gv}, job, samples, stats, err,
+                                          work);
+    } else if constexpr (kLds == 6) {
+        for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
+        __syncthreads();
+        MM_TS_STAGED();
+        const auto v = view(SplitNodes{lds, sc.nodes, sc.n_lds_f4}, sc.recs);
+        chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats, err,
+                                          work);
+    } else if constexpr (kLds == 10) {
+        float* tab = reinterpret_cast<float*>(lds);
         uint32_t* words = reinterpret_cast<uint32_t*>(tab + 256);
         for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = sc.dict_tab[i];
         for (uint32_t i = threadIdx.x; i < 3 * sc.n_nodes; i += blockDim.x) words[i] = sc.dict_words[i];
         __syncthreads();
         MM_TS_STAGED();
-        WpStack<kWW> st;
-        chunks = wp_dispatch<kStats, kWW>(sc, view(DictNodes{words, tab}, sc.recs), st, job, samples, stats, err,
+        const auto v = view(DictNodes{words, tab}, sc.recs);
+        chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats, err,
                                           work);
-    } else if constexpr (kLds == 7) {
-        extern __shared__ float4 lds_nodes7[];
-        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes7[i] = sc.nodes[i];
-        __syncthreads();
-        MM_TS_STAGED();
-        WpStack<kWW> st;
-        chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes7, sc.recs), st, job, samples, stats, err, work);
-    } else if constexpr (kLds > 0) {
-        extern __shared__ float4 lds_nodes[];
-        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
-        uint2* lds_recs = reinterpret_cast<uint2*>(lds_nodes + 2 * sc.n_nodes);
-        if constexpr (kLds == 3 || kLds == 9)
+    } else if constexpr (kLds == 1 || kLds == 3 || kLds == 7) {
+        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds[i] = sc.nodes[i];
+        uint2* lds_recs = reinterpret_cast<uint2*>(lds + 2 * sc.n_nodes);
+        if constexpr (kLds == 3)
             for (uint32_t i = threadIdx.x; i < 5 * sc.n_rects; i += blockDim.x) lds_recs[i] = sc.recs[i];
         __syncthreads();
         MM_TS_STAGED();
         if constexpr (kLds == 3) {
-            WpStack<kWW> st;
-            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
-        } else if constexpr (kLds == 9) {  // = 3 with u16 stack entries in scratch
-            ScratchStack16 st;
-            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, lds_recs), st, job, samples, stats, err, work);
-        } else if constexpr (kLds == 5) {
-            WpStack<kWW> st;
-            const LdsCold cold{reinterpret_cast<float*>(lds_recs) + threadIdx.x, blockDim.x};
-            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work, cold);
-        } else if constexpr (kLds == 2 || kLds == 8) {
-            LdsStack16 st;
-            st.base = reinterpret_cast<uint16_t*>(lds_recs) + threadIdx.x;
-            st.stride = blockDim.x;
-            st.cap = stack_slots;
-            if constexpr (kLds == 8)  // + compact rect records through L1/L2
-                chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes, sc.recs), st, job, samples, stats, err, work);
-            else
-                chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            const auto v = view(static_cast<float4*>(lds), lds_recs);
+            chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats,
+                                              err, work);
+        } else if constexpr (kLds == 7) {
+            const auto v = view(static_cast<float4*>(lds), sc.recs);
+            chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats,
+                                              err, work);
         } else {
-            WpStack<kWW> st;
-            chunks = wp_dispatch<kStats, kWW>(sc, view(lds_nodes), st, job, samples, stats, err, work);
+            const auto v = view(static_cast<float4*>(lds));
+            chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats,
+                                              err, work);
         }
     } else {
-        WpStack<kWW> st;
-        chunks = wp_dispatch<kStats, kWW>(sc, view(sc.nodes), st, job, samples, stats, err, work);
+        const auto v = view(sc.nodes);
+        chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats, err,
+                                          work);
     }
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -415,67 +306,50 @@ __global__ __launch_bounds__(kBlock, kMinWaves) void k_trace_wavepersist(DevScen
     }
 }
 
-template <int kLds, int kBlock, int kMinWaves, int kWW>
+size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
+    switch (lds_mode) {
+        case 11: return sc.grid.bytes;
+        case 12: return sc.grid.off_recs;
+        case 6: return (size_t)sc.n_lds_f4 * sizeof(float4);
+        case 10: return 256 * sizeof(float) + 3 * (size_t)sc.n_nodes * sizeof(uint32_t);
+        case 1: case 7: return 2 * (size_t)sc.n_nodes * sizeof(float4);
+        case 3: return 2 * (size_t)sc.n_nodes * sizeof(float4) + 5 * (size_t)sc.n_rects * sizeof(uint2);
+        default: return 0;
+    }
+}
+
+template <int kLds, int kForm>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
-                                       uint32_t stack_slots, hipStream_t s) {
-    const uint32_t block = kBlock;
-    const size_t lds = kLds == 10 ? 256 * sizeof(float) + 3 * (size_t)sc.n_nodes * sizeof(uint32_t)
-                     : (kLds == 4 || kLds == 6) ? (size_t)sc.n_lds_f4 * sizeof(float4)
-                                 : (kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0) +
-                                       (kLds == 5 ? 6 * (size_t)block * sizeof(float) : 0) +
-                                       (kLds == 2 || kLds == 8 ? (size_t)stack_slots * block * sizeof(uint16_t) : 0) +
-                                       (kLds == 3 || kLds == 9 ? 5 * (size_t)sc.n_rects * sizeof(uint2) : 0);
-    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kBlock, kMinWaves, kWW>
-                            : k_trace_wavepersist<false, kLds, kBlock, kMinWaves, kWW>;
+                                       hipStream_t s) {
+    constexpr uint32_t block = 1024;
+    const size_t lds = wavepersist_lds_bytes(sc, kLds);
+    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm> : k_trace_wavepersist<false, kLds, kForm>;
     int per_cu = 0, dev = 0, cus = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
     if (e != hipSuccess) return e;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t n_paths = job.w * job.h * job.e.spp;
+    const uint64_t n_paths = (uint64_t)job.w * job.h * job.e.spp * job.n_frames;
     // MM_OPT_RESERVE_CUS: leave that many CUs' worth of resident blocks free for other work (collectives)
     const int cus_used = std::max(1, cus - (int)job.reserve_cus);
-    uint32_t grid = (uint32_t)std::max(1, per_cu) * (uint32_t)cus_used;
-    grid = std::max(1u, std::min(grid, (n_paths + block - 1) / block));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, s, sc, job, samples, stats, err, work, stack_slots);
+    uint64_t grid = (uint64_t)std::max(1, per_cu) * (uint64_t)cus_used;
+    grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, (n_paths + block - 1) / block));
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(block), lds, s, sc, job, samples, stats, err, work);
     return hipGetLastError();
 }
 
-// Register budget by launch bounds: waves/SIMD = 8 -> <= 64 VGPRs.
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
-                                    int lds_mode, uint32_t stack_slots, uint32_t block, uint32_t min_waves,
-                                    int loop_form, hipStream_t s) {
-#define MM_WP2(L, B, W, WW) \
-    if (lds_mode == L) return launch_wavepersist_t<L, B, W, WW>(sc, job, samples, stats, err, work, count_stats, stack_slots, s);
-#define MM_WP3(B, W, WW) \
-    if (loop_form == WW) { MM_WP2(3, B, W, WW) MM_WP2(2, B, W, WW) MM_WP2(1, B, W, WW) MM_WP2(0, B, W, WW) }
-#define MM_WP(B, W) \
-    if (block == B && min_waves == W) {                                                              \
-        if (loop_form == 0) { MM_WP2(4, B, W, 0) }                                                    \
-        if (loop_form == 2) { MM_WP2(4, B, W, 2) }                                                    \
-        if (loop_form == 3) { MM_WP2(4, B, W, 3) }                                                    \
-        if (loop_form == 0) { MM_WP2(5, B, W, 0) MM_WP2(6, B, W, 0) MM_WP2(7, B, W, 0) }              \
-        if (loop_form == 4) { MM_WP2(4, B, W, 4) MM_WP2(3, B, W, 4) MM_WP2(1, B, W, 4) MM_WP2(0, B, W, 4) }  \
-        MM_WP3(B, W, 0) MM_WP3(B, W, 1) MM_WP3(B, W, 2) MM_WP3(B, W, 3) MM_WP3(B, W, 8) MM_WP3(B, W, 16)  \
-        MM_WP3(B, W, 32) }
-    MM_WP(256, 8) MM_WP(512, 6) MM_WP(512, 8) MM_WP(1024, 1) MM_WP(1024, 8)
-    if (block == 1024 && min_waves == 8 && loop_form == 5) {
-        MM_WP2(4, 1024, 8, 5) MM_WP2(6, 1024, 8, 5) MM_WP2(7, 1024, 8, 5) MM_WP2(8, 1024, 8, 5) MM_WP2(9, 1024, 8, 5)
-        MM_WP2(10, 1024, 8, 5)
-        MM_WP3(1024, 8, 5)
-    }
-    if (block == 1024 && min_waves == 8 && loop_form == 6) { MM_WP2(3, 1024, 8, 6) MM_WP2(4, 1024, 8, 6) }
-    if (block == 1024 && min_waves == 8 && loop_form == 7) {
-        MM_WP2(3, 1024, 8, 7) MM_WP2(6, 1024, 8, 7) MM_WP2(7, 1024, 8, 7) MM_WP2(10, 1024, 8, 7)
-    }
-    if (block == 1024 && min_waves == 8 && loop_form == 9) { MM_WP2(3, 1024, 8, 9) MM_WP2(6, 1024, 8, 9) MM_WP2(7, 1024, 8, 9) }
-    // 768-thread blocks at 6 waves/SIMD (80 VGPRs): two blocks per CU still fit the LDS
-    if (block == 768 && min_waves == 6 && loop_form == 5) { MM_WP2(3, 768, 6, 5) MM_WP2(6, 768, 6, 5) }
+                                    int lds_mode, int form, hipStream_t s) {
+#define MM_WP(L, F) \
+    if (lds_mode == L && form == F) return launch_wavepersist_t<L, F>(sc, job, samples, stats, err, work, count_stats, s);
+    MM_WP(11, kFormGrid) MM_WP(12, kFormGrid) MM_WP(13, kFormGrid)
+    MM_WP(3, kFormLean) MM_WP(6, kFormLean) MM_WP(7, kFormLean) MM_WP(10, kFormLean)
+    MM_WP(0, kFormLeafInterior) MM_WP(1, kFormLeafInterior) MM_WP(3, kFormLeafInterior) MM_WP(6, kFormLeafInterior)
+    MM_WP(7, kFormLeafInterior) MM_WP(10, kFormLeafInterior)
+    MM_WP(1, kFormIfIf) MM_WP(3, kFormIfIf)
 #undef MM_WP
-#undef MM_WP3
-#undef MM_WP2
     return hipErrorInvalidValue;
 }
 
@@ -499,20 +373,6 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
         launch_mega_t<false, true>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
     else
         launch_mega_t<false, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Tail gate: a one-wave no-op queued ahead of a frame's trace kernel when
-// frames from several contexts share the GPU.  It can only be dispatched once
-// a wave slot frees up, i.e. once the frame already running starts to drain,
-// so the next frame's resident blocks fill exactly the CUs the previous
-// frame's tail leaves idle instead of splitting the GPU with it from the start
-// (measured: profiles/r01_overlap_probe.txt).
-__global__ void k_tail_gate() {}
-
-hipError_t launch_tail_gate(hipStream_t s) {
-    hipLaunchKernelGGL(k_tail_gate, dim3(1), dim3(64), 0, s);
     return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "mm_launch.h"
-#include "mm_trace.h"
+#include "mm_path.h"
 
 namespace mm {
 
@@ -105,7 +105,7 @@ __device__ __forceinline__ void extend_body(const DevScene& sc, const V& v, cons
         float t = kBig;
         uint32_t k = 0;
         ScratchStack stack;
-        const bool ok = closest_hit<kStats>(sc, v, o, d, t, k, stack, c);
+        const bool ok = closest_hit_bvh<kStats, kFormIfIf>(sc, v, make_ray(o, d), t, k, stack, c);
         if (kStats) c.rays++;
         ws.hit_t[pid] = t;
         ws.hit_i[pid] = ok ? k : kHitOverflow;

@@ -33,10 +33,11 @@ MM_OK, MM_ERR_INVALID, MM_ERR_HIP, MM_ERR_NOMEM = 0, -1, -2, -3
 MM_ERR_NO_SCENE, MM_ERR_STACK, MM_ERR_UNSUPPORTED = -4, -5, -6
 MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE = 0x1, 0x2
 MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2, 3
-MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_THRESHOLD, MM_OPT_MIN_WAVES, MM_OPT_LDS_STACK = 1, 2, 3, 4, 5, 6
-MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS, MM_OPT_LDS_SPLIT, MM_OPT_COLD_LDS, MM_OPT_GLOBAL_RECTS = 7, 8, 9, 10, 11
-MM_OPT_FUSE_RESOLVE, MM_OPT_TAIL_GATE, MM_OPT_FAIR, MM_OPT_GRAB, MM_OPT_BLOCKSYNC = 12, 13, 14, 15, 16
-MM_OPT_CHUNK_ORDER, MM_OPT_RESERVE_CUS, MM_OPT_DICT_NODES = 17, 19, 20
+MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS = 1, 2, 3, 7, 8
+MM_OPT_LDS_SPLIT, MM_OPT_FUSE_RESOLVE, MM_OPT_RESERVE_CUS, MM_OPT_DICT_NODES = 9, 12, 19, 20
+MM_TRAV_AUTO, MM_TRAV_IFIF, MM_TRAV_LEAF_INTERIOR, MM_TRAV_LEAN, MM_TRAV_GRID = -1, 0, 5, 7, 11
+MM_INFO_GRID_OK, MM_INFO_GRID_CELLS_X, MM_INFO_GRID_CELLS_Y, MM_INFO_GRID_CELLS_Z = 1, 2, 3, 4
+MM_INFO_GRID_GLOBAL, MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_LEAN, MM_INFO_DEPTH = 5, 6, 7, 8, 9
 MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
@@ -108,6 +109,7 @@ EXPORTS = {
                                        C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, C.POINTER(mm_stats)]),
     "mm_set_pipeline": (C.c_int, [P, C.c_int]),
     "mm_set_option": (C.c_int, [P, C.c_int, C.c_int]),
+    "mm_scene_info": (C.c_int, [P, C.c_int, C.POINTER(C.c_double)]),
     "mm_set_wave_timeline": (C.c_int, [P, P, C.c_uint32]),
     "mm_sync": (C.c_int, [P]),
     "mm_last_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),

@@ -86,6 +86,13 @@ class Renderer:
     def set_option(self, key: int, value: int) -> None:
         self._check(lib().mm_set_option(self._ctx, key, value))
 
+    def scene_info(self, key: int) -> float:
+        """mm_scene_info: facts about the uploaded scene's search structures
+        (MM_INFO_*: grid availability and size, BVH depth)."""
+        v = C.c_double()
+        self._check(lib().mm_scene_info(self._ctx, key, C.byref(v)))
+        return v.value
+
     # -- scene ------------------------------------------------------------
     def upload_scene(self, s: Scene) -> None:
         rects = np.ascontiguousarray(s.rects, dtype=np.float32)

@@ -1,0 +1,343 @@
+/*
+ * grid_sim.c — CPU experiment: closest-hit queries answered by a uniform-grid
+ * search + exact verification, checked against the reference traversal
+ * (oracle/mm_oracle.c's intersect_bvh) on every query of real C3 paths.
+ *
+ * Build: gcc -O2 -fopenmp -ffp-contract=off -o /tmp/sim/grid_sim scripts/grid_sim.c -lm
+ * Run:   /tmp/sim/grid_sim /tmp/sim/scene32.bin W H spp bl ml rows_step
+ *
+ * The scene file holds n_rects, n_nodes, rects (48 B), nodes (32 B), idx,
+ * is_mirror, emission (see the session notes in DESIGN.md).
+ */
+#include "../oracle/mm_oracle.c"
+
+#include <stdio.h>
+#include <float.h>
+
+/* ---------------------------------------------------------------- scene */
+static oracle_scene S;
+static uint32_t* leaf_of_rect;   /* rect index -> reference leaf node */
+
+static void load(const char* path) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { perror(path); exit(1); }
+    uint32_t nn[2];
+    if (fread(nn, 4, 2, f) != 2) exit(1);
+    S.n_rects = nn[0]; S.n_nodes = nn[1];
+    mm_rect* r = malloc(sizeof(mm_rect) * S.n_rects);
+    mm_node* n = malloc(sizeof(mm_node) * S.n_nodes);
+    uint32_t* idx = malloc(4 * S.n_rects);
+    uint8_t* m = malloc(S.n_rects);
+    float* e = malloc(16 * S.n_rects);
+    if (fread(r, sizeof(mm_rect), S.n_rects, f) != S.n_rects) exit(1);
+    if (fread(n, sizeof(mm_node), S.n_nodes, f) != S.n_nodes) exit(1);
+    if (fread(idx, 4, S.n_rects, f) != S.n_rects) exit(1);
+    if (fread(m, 1, S.n_rects, f) != S.n_rects) exit(1);
+    if (fread(e, 16, S.n_rects, f) != S.n_rects) exit(1);
+    fclose(f);
+    S.rects = r; S.nodes = n; S.idx = idx; S.is_mirror = m; S.emission = e;
+    leaf_of_rect = malloc(4 * S.n_rects);
+    for (uint32_t i = 0; i < S.n_nodes; ++i)
+        if (n[i].count)
+            for (uint32_t j = 0; j < n[i].count; ++j) leaf_of_rect[idx[n[i].left_first + j]] = i;
+}
+
+/* ---------------------------------------------------------------- grid */
+static float gmin[3], gcell[3], ginv[3], geps;
+static int gn[3];
+static uint32_t* cell_off;   /* n_cells + 1 */
+static uint32_t* cell_list;
+static uint32_t* glob; static uint32_t n_glob;
+
+static void rect_box(const mm_rect* r, double lo[3], double hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        double c[4] = {r->o[a], (double)r->o[a] + r->v[a], (double)r->o[a] + r->u[a],
+                       (double)r->o[a] + r->v[a] + r->u[a]};
+        lo[a] = hi[a] = c[0];
+        for (int k = 1; k < 4; ++k) { if (c[k] < lo[a]) lo[a] = c[k]; if (c[k] > hi[a]) hi[a] = c[k]; }
+    }
+}
+
+static int cmpf(const void* a, const void* b) {
+    float x = *(const float*)a, y = *(const float*)b;
+    return (x > y) - (x < y);
+}
+
+static void build_grid(double cell_target) {
+    double smin[3] = {1e30, 1e30, 1e30}, smax[3] = {-1e30, -1e30, -1e30}, C = 1.0;
+    for (uint32_t k = 0; k < S.n_rects; ++k) {
+        double lo[3], hi[3];
+        rect_box(&S.rects[k], lo, hi);
+        for (int a = 0; a < 3; ++a) {
+            if (lo[a] < smin[a]) smin[a] = lo[a];
+            if (hi[a] > smax[a]) smax[a] = hi[a];
+            if (fabs(lo[a]) > C) C = fabs(lo[a]);
+            if (fabs(hi[a]) > C) C = fabs(hi[a]);
+        }
+    }
+    geps = (float)(C * 0x1p-14);
+    if (cell_target <= 0) {  /* median of the rects' smaller nonzero extent */
+        float* ext = malloc(4 * S.n_rects);
+        uint32_t m = 0;
+        for (uint32_t k = 0; k < S.n_rects; ++k) {
+            double lo[3], hi[3];
+            rect_box(&S.rects[k], lo, hi);
+            double e1 = 0, e2 = 0;
+            for (int a = 0; a < 3; ++a) {
+                double e = hi[a] - lo[a];
+                if (e > e1) { e2 = e1; e1 = e; } else if (e > e2) e2 = e;
+            }
+            if (e2 > 0) ext[m++] = (float)e2;
+        }
+        qsort(ext, m, 4, cmpf);
+        cell_target = ext[m / 2];
+        free(ext);
+    }
+    long total = 1;
+    for (int a = 0; a < 3; ++a) {
+        double lo = smin[a] - geps, hi = smax[a] + geps;
+        int n = (int)floor((hi - lo) / cell_target + 0.5);
+        if (n < 1) n = 1;
+        if (n > 256) n = 256;
+        gn[a] = n;
+        gmin[a] = (float)lo;
+        gcell[a] = (float)((hi - lo) / n);
+        ginv[a] = 1.0f / gcell[a];
+        total *= n;
+    }
+    /* global rects: cover more than half of the cells */
+    glob = malloc(4 * S.n_rects);
+    uint32_t* cnt = calloc(total + 1, 4);
+    uint8_t* is_glob = calloc(S.n_rects, 1);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (uint32_t k = 0; k < S.n_rects; ++k) {
+            double lo[3], hi[3];
+            rect_box(&S.rects[k], lo, hi);
+            int i0[3], i1[3];
+            long cover = 1;
+            for (int a = 0; a < 3; ++a) {
+                i0[a] = (int)floor((lo[a] - geps - gmin[a]) / gcell[a]);
+                i1[a] = (int)floor((hi[a] + geps - gmin[a]) / gcell[a]);
+                if (i0[a] < 0) i0[a] = 0;
+                if (i1[a] > gn[a] - 1) i1[a] = gn[a] - 1;
+                cover *= (i1[a] - i0[a] + 1);
+            }
+            if (pass == 0) {
+                if (cover * 2 > total) { is_glob[k] = 1; glob[n_glob++] = k; continue; }
+            } else if (is_glob[k]) continue;
+            for (int z = i0[2]; z <= i1[2]; ++z)
+                for (int y = i0[1]; y <= i1[1]; ++y)
+                    for (int x = i0[0]; x <= i1[0]; ++x) {
+                        long c = ((long)z * gn[1] + y) * gn[0] + x;
+                        if (pass == 0) cnt[c + 1]++;
+                        else cell_list[cnt[c]++] = k;
+                    }
+        }
+        if (pass == 0) {
+            for (long c = 0; c < total; ++c) cnt[c + 1] += cnt[c];
+            cell_off = malloc(4 * (total + 1));
+            memcpy(cell_off, cnt, 4 * (total + 1));
+            cell_list = malloc(4 * (cnt[total] + 1));
+        }
+    }
+    fprintf(stderr, "grid %d x %d x %d, cell (%g %g %g), eps %g, %u global, %u list entries (%.2f/cell)\n",
+            gn[0], gn[1], gn[2], gcell[0], gcell[1], gcell[2], geps, n_glob, cell_off[total],
+            (double)cell_off[total] / total);
+    free(cnt);
+    free(is_glob);
+}
+
+/* ---------------------------------------------------------------- queries */
+/* reference rect test without the a < t clause: a, or BIG */
+static inline float rect_a(v3 ori, v3 dir, const mm_rect* r) {
+    v3 o = ld3(r->o), v = ld3(r->v), u = ld3(r->u);
+    v3 n = normalize3(cross3(v, u));
+    float nc = dot3(dir, n);
+    float a = dot3(vsub(o, ori), n) / nc;
+    v3 rv = vadd(vsub(ori, o), vscale(a, dir));
+    float lv = sqrtf(dot3(v, v));
+    float d1 = dot3(rv, v) / lv;
+    float lu = sqrtf(dot3(u, u));
+    float d2 = dot3(rv, u) / lu;
+    if (d1 >= 0.0f && d1 <= lv && d2 >= 0.0f && d2 <= lu && nc != 0.0f && a > 0.1f) return a;
+    return BIG;
+}
+
+typedef struct {
+    uint64_t queries, cells, tests, fallback_tie, fallback_verify, fallback_guard, mismatch, miss;
+    uint64_t hist_cells[64];
+} gstats;
+
+static inline void consider(float a, uint32_t k, float* best, uint32_t* bk, int* tie) {
+    if (a == BIG) return;
+    if (a < *best) { *best = a; *bk = k; *tie = 0; }
+    else if (a == *best && k != *bk) *tie = 1;
+}
+
+/* grid search + verification; returns 1 and (t, index) when certified */
+static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
+    float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, yy[3];
+    for (int a = 0; a < 3; ++a) {
+        float ad = fabsf(dd[a]);
+        if (!(ad >= 0x1p-40f && ad <= 0x1p40f)) { st->fallback_guard++; return 0; }
+        if (oo[a] < gmin[a] || oo[a] > gmin[a] + gcell[a] * gn[a]) { st->fallback_guard++; return 0; }
+        yy[a] = 1.0f / dd[a];
+    }
+    float best = BIG;
+    uint32_t bk = 0;
+    int tie = 0;
+    for (uint32_t j = 0; j < n_glob; ++j) { consider(rect_a(o, d, &S.rects[glob[j]]), glob[j], &best, &bk, &tie); st->tests++; }
+    int ic[3], stp[3];
+    float tn[3];
+    for (int a = 0; a < 3; ++a) {
+        int i = (int)floorf((oo[a] - gmin[a]) * ginv[a]);
+        if (i < 0) i = 0;
+        if (i > gn[a] - 1) i = gn[a] - 1;
+        ic[a] = i;
+        stp[a] = dd[a] > 0.0f ? 1 : -1;
+        tn[a] = (gmin[a] + (float)(i + (stp[a] > 0)) * gcell[a] - oo[a]) * yy[a];
+    }
+    int ncell = 0;
+    for (;;) {
+        long c = ((long)ic[2] * gn[1] + ic[1]) * gn[0] + ic[0];
+        ncell++;
+        for (uint32_t j = cell_off[c]; j < cell_off[c + 1]; ++j) {
+            uint32_t k = cell_list[j];
+            consider(rect_a(o, d, &S.rects[k]), k, &best, &bk, &tie);
+            st->tests++;
+        }
+        int a = tn[0] <= tn[1] ? (tn[0] <= tn[2] ? 0 : 2) : (tn[1] <= tn[2] ? 1 : 2);
+        if (best < tn[a]) break;
+        ic[a] += stp[a];
+        if (ic[a] < 0 || ic[a] >= gn[a]) break;
+        tn[a] = (gmin[a] + (float)(ic[a] + (stp[a] > 0)) * gcell[a] - oo[a]) * yy[a];
+    }
+    st->cells += ncell;
+    st->hist_cells[ncell < 63 ? ncell : 63]++;
+    if (best == BIG) { st->miss++; *t_out = BIG; *i_out = 0; return 1; }
+    if (tie) { st->fallback_tie++; return 0; }
+    /* the reference leaf of bk passes at every t > best */
+    const mm_node* L = &S.nodes[leaf_of_rect[bk]];
+    ray_t b; b.ori = o; b.dir = d; b.t = BIG; b.index = 0;
+    float tx1 = (L->mn[0] - o.x) / d.x, tx2 = (L->mx[0] - o.x) / d.x;
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    float ty1 = (L->mn[1] - o.y) / d.y, ty2 = (L->mx[1] - o.y) / d.y;
+    tmin = fmaxf(tmin, fminf(ty1, ty2)); tmax = fminf(tmax, fmaxf(ty1, ty2));
+    float tz1 = (L->mn[2] - o.z) / d.z, tz2 = (L->mx[2] - o.z) / d.z;
+    tmin = fmaxf(tmin, fminf(tz1, tz2)); tmax = fminf(tmax, fmaxf(tz1, tz2));
+    (void)b;
+    if (!(tmax >= tmin && tmax > 0.0f && tmin <= best)) { st->fallback_verify++; return 0; }
+    *t_out = best;
+    *i_out = bk;
+    return 1;
+}
+
+/* the reference path loop with every query cross-checked */
+static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t* tr, uint64_t* rays) {
+    ray_t b;
+    b.ori = ori; b.dir = dir; b.t = BIG; b.index = 0;
+    v3 T = mk(1, 1, 1), L = mk(0, 0, 0);
+    int mh = 0;
+    for (int n = 0; n < bl + mh; ++n) {
+        intersect_bvh(&b, &S, tr);
+        (*rays)++;
+        float gt; uint32_t gi;
+        st->queries++;
+        if (grid_query(b.ori, b.dir, &gt, &gi, st)) {
+            if (gt != b.t || (gt < BIG && gi != b.index)) {
+                st->mismatch++;
+                if (st->mismatch < 10)
+                    fprintf(stderr, "MISMATCH o=(%a %a %a) d=(%a %a %a) ref t=%a k=%u grid t=%a k=%u\n", b.ori.x, b.ori.y,
+                            b.ori.z, b.dir.x, b.dir.y, b.dir.z, b.t, b.index, gt, gi);
+            }
+        }
+        if (!(b.t < BIG)) break;
+        const uint32_t k = b.index;
+        const mm_rect* r = &S.rects[k];
+        v3 nn = normalize3(cross3(ld3(r->v), ld3(r->u)));
+        float sg = msign(dot3(b.dir, nn));
+        float side = -sg;
+        if (S.is_mirror[k] == 0 || sg == 1.0f) {
+            const float* e = &S.emission[4 * k];
+            v3 contrib = vmul(vscale(e[3], T), ld3(e));
+            v3 newT = vmul(ld3(r->color), T);
+            float rx = oracle_rand_pm1(&seed), ry = oracle_rand_pm1(&seed), rz = oracle_rand_pm1(&seed);
+            v3 rd = mk(rx, ry, rz);
+            float len2 = dot3(rd, rd);
+            while (sqrtf(len2) > 1.0f) {
+                rx = oracle_rand_pm1(&seed); ry = oracle_rand_pm1(&seed); rz = oracle_rand_pm1(&seed);
+                rd = mk(rx, ry, rz);
+                len2 = dot3(rd, rd);
+            }
+            v3 rn = vscale(rsq(len2), rd);
+            b.ori = vadd(b.ori, vscale(b.t, b.dir));
+            v3 nd = vadd(rn, vscale(side, nn));
+            b.dir = vscale(rsq(dot3(nd, nd)), nd);
+            L = vadd(contrib, L);
+            T = newT;
+        } else {
+            if (mh + 1 < ml) {
+                v3 contrib = vscale(0.005f, ld3(r->color));
+                b.ori = vadd(b.ori, vscale(b.t, b.dir));
+                float dd = dot3(nn, b.dir) * 2.0f;
+                v3 rf = vsub(b.dir, vscale(dd, nn));
+                b.dir = vscale(rsq(dot3(rf, rf)), rf);
+                L = vadd(contrib, L);
+                mh = mh + 1;
+            } else break;
+        }
+        b.t = BIG;
+    }
+    return L;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 8) { fprintf(stderr, "usage: grid_sim scene W H spp bl ml rowstep [cell]\n"); return 1; }
+    load(argv[1]);
+    int W = atoi(argv[2]), H = atoi(argv[3]), spp = atoi(argv[4]), bl = atoi(argv[5]), ml = atoi(argv[6]);
+    int rs = atoi(argv[7]);
+    build_grid(argc > 8 ? atof(argv[8]) : 0.0);
+    mm_uniform u;
+    /* default camera (mm_uniform_default): centre (-5,0,-45), quat from (0.1,0,1), focal 1, viewport (2W/H, 2) */
+    u.cam.center[0] = -5.0f; u.cam.center[1] = 0.0f; u.cam.center[2] = -45.0f; u.cam.focal = 1.0f;
+    u.cam.quat[0] = 0.0f; u.cam.quat[1] = 0.04981370270252228f; u.cam.quat[2] = 0.0f; u.cam.quat[3] = 0.9987585544586182f;
+    u.cam.viewport[0] = 2.0f * (float)W / (float)H; u.cam.viewport[1] = 2.0f;
+    u.view_w = (float)W; u.view_h = (float)H; u.chunk_w = 4; u.time = 0;
+    gstats tot;
+    memset(&tot, 0, sizeof tot);
+    uint64_t rays_tot = 0;
+#pragma omp parallel
+    {
+        gstats st;
+        memset(&st, 0, sizeof st);
+        trav_t tr = {0, 0, 0};
+        uint64_t rays = 0;
+#pragma omp for schedule(dynamic, 1)
+        for (int y = 0; y < H; y += rs)
+            for (int x = 0; x < W; ++x) {
+                v3 d0 = primary_dir(&u, x, y);
+                for (int k = 0; k < spp; ++k) {
+                    uint32_t seed = oracle_tile_seed(y * W + x, k, 0);
+                    v3 d = jittered_dir(d0, &seed);
+                    path(ld3(u.cam.center), d, seed, bl, ml, &st, &tr, &rays);
+                }
+            }
+#pragma omp critical
+        {
+            tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
+            tot.fallback_tie += st.fallback_tie; tot.fallback_verify += st.fallback_verify;
+            tot.fallback_guard += st.fallback_guard; tot.mismatch += st.mismatch; tot.miss += st.miss;
+            for (int i = 0; i < 64; ++i) tot.hist_cells[i] += st.hist_cells[i];
+            rays_tot += rays;
+        }
+    }
+    double q = (double)tot.queries;
+    printf("queries %llu  cells/query %.3f  rect tests/query %.3f  fallback tie %.5f%% verify %.5f%% guard %.5f%%  miss %llu  MISMATCH %llu\n",
+           (unsigned long long)tot.queries, tot.cells / q, tot.tests / q, 100 * tot.fallback_tie / q,
+           100 * tot.fallback_verify / q, 100 * tot.fallback_guard / q, (unsigned long long)tot.miss,
+           (unsigned long long)tot.mismatch);
+    printf("cells hist:");
+    for (int i = 1; i < 40; ++i) printf(" %d:%.3f", i, tot.hist_cells[i] / q);
+    printf("\n");
+    return tot.mismatch ? 2 : 0;
+}

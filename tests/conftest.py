@@ -51,3 +51,35 @@ def gpu():
 
     torch.cuda.init()
     return torch.device("cuda:0")
+
+
+def host_threads() -> int:
+    """Worker threads for CPU-side oracle runs: the usable CPUs of this
+    process, capped at 16 (a GPU box's CPU share per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def oracle_tile(o, uniform, ext, x0, y0, w, h, y_stride=1, threads=None):
+    """oracle_trace_tile over a thread pool (the C call releases the GIL): the
+    tile's rows in bands, bit-identical to one call (each pixel's value
+    depends on its own (pixel, sample, frame) only).  Returns (out, rays)."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+
+    threads = threads or host_threads()
+    out = np.zeros((h, w, 4), dtype=np.float32)
+    band = max(1, -(-h // (4 * threads)))
+    jobs = [(j0, min(band, h - j0)) for j0 in range(0, h, band)]
+
+    def run(job):
+        j0, n = job
+        part, st = o.trace_tile(uniform, ext, x0, y0 + j0 * y_stride, w, n, y_stride=y_stride, out=out[j0:j0 + n])
+        return st.rays
+
+    with ThreadPoolExecutor(threads) as ex:
+        rays = sum(ex.map(run, jobs))
+    return out, rays

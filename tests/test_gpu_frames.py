@@ -1,0 +1,147 @@
+"""Whole-frame parity on the paths bench.py times: the HIP output of entire
+C2 / C3 frames, of rank 0's row set of an 8-way C4 split, and of C5 windows at
+64 spp (single frames and 3-frame temporal accumulation) against the CPU
+oracle, bit for bit.  The oracle runs over a thread pool on the host's CPUs
+(conftest.oracle_tile).  Reference: src/shaders.metal:245-368 (the kernel),
+342-364 (the 64-sample reduction), src/main.rs:778-784 (temporal refresh)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import oracle_tile
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _scene(n):
+    from mirror_maze import Scene
+
+    return Scene.build(n, 0)
+
+
+def _diff(got, ref):
+    bad = (_bits(got) != _bits(ref)).any(axis=-1)
+    return int(bad.sum())
+
+
+def test_c3_bench_path_two_whole_frames(gpu):
+    """C3 exactly as bench.py renders it: MM_PIPE_AUTO (the grid search), two
+    consecutive frames in ONE mm_trace_tile_frames launch, every pixel of
+    both 1920x1080 frames (2 x 137 M closest-hit queries) vs the oracle."""
+    from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(32)
+    r = Renderer(0)
+    r.set_pipeline(MM_PIPE_AUTO)
+    r.upload_scene(s)
+    u = default_uniform(1920, 1080, 0)
+    e = make_ext(8, 8, 8, frame=0)
+    got, st = r.trace_tile_frames(u, e, 2, 0, 0, 1920, 1080, stats=True)
+    got = got.cpu().numpy()
+    o = Oracle.from_scene(s)
+    rays = 0
+    for f in range(2):
+        ref, n = oracle_tile(o, u, make_ext(8, 8, 8, frame=f), 0, 0, 1920, 1080)
+        rays += n
+        assert _diff(got[f], ref) == 0, f"frame {f}: {_diff(got[f], ref)} pixels differ"
+    assert st.rays == rays
+    r.close()
+
+
+def test_c2_whole_frame(gpu):
+    """C2: 16x16 maze, 1920x1080, 1 spp, 4/15 bounces, the whole frame."""
+    from mirror_maze import Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(16)
+    r = Renderer(0)
+    r.upload_scene(s)
+    u = default_uniform(1920, 1080, 0)
+    e = make_ext(1, 4, 15, frame=0)
+    got, st = r.trace_tile(u, e, 0, 0, 1920, 1080, stats=True)
+    ref, rays = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 1920, 1080)
+    assert _diff(got.cpu().numpy(), ref) == 0
+    assert st.rays == rays
+    r.close()
+
+
+def test_c4_rank0_of_eight_way_split(gpu):
+    """C4 (32x32 maze, 3840x2160, 16 spp, 8/15 bounces): rank 0's rows of the
+    8-way interleaved split (mirror_maze.dist.row_shard), as an 8-GPU run
+    renders them, vs the oracle on the same rows."""
+    from mirror_maze import Renderer, default_uniform, make_ext
+    from mirror_maze.dist import row_shard
+    from oracle.oracle import Oracle
+
+    s = _scene(32)
+    r = Renderer(0)
+    r.upload_scene(s)
+    W, H = 3840, 2160
+    y0, stride, rows = row_shard(H, 8, 0)
+    u = default_uniform(W, H, 0)
+    e = make_ext(16, 8, 15, frame=0)
+    got, st = r.trace_tile(u, e, 0, y0, W, rows, y_stride=stride, stats=True)
+    ref, rays = oracle_tile(Oracle.from_scene(s), u, e, 0, y0, W, rows, y_stride=stride)
+    assert _diff(got.cpu().numpy(), ref) == 0
+    assert st.rays == rays
+    r.close()
+
+
+C5_WINDOWS = [(0, 0), (1904, 1064), (3808, 2144), (700, 1500), (2900, 300), (1200, 40)]
+
+
+@pytest.mark.parametrize("opts", [{}, {7: 7}], ids=["auto", "bvh-lean-dict"])
+def test_c5_windows_64spp(gpu, opts):
+    """C5: 64x64 maze, 3840x2160 frame coordinates, 64 spp, 16/16 bounces --
+    the reference's 64-sample reduction (shaders.metal:342-364) as the fused
+    resolve, one pixel per wave -- on six 32x16 windows."""
+    from mirror_maze import Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(64)
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload_scene(s)
+    u = default_uniform(3840, 2160, 0)
+    e = make_ext(64, 16, 16, frame=7)
+    for (x0, y0) in C5_WINDOWS:
+        got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
+        ref, rays = oracle_tile(o, u, e, x0, y0, 32, 16)
+        assert _diff(got.cpu().numpy(), ref) == 0, (x0, y0)
+        assert st.rays == rays
+    r.close()
+
+
+def test_c5_temporal_accumulation_three_frames(gpu):
+    """C5's temporal accumulation (MM_EXT_ACCUMULATE: every frame adds its
+    per-pixel 64-spp mean into one running sum, alpha counts frames) over
+    frames 0, 1, 2 on two windows and a row band, vs the oracle's accumulate."""
+    from mirror_maze import MM_EXT_ACCUMULATE, Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(64)
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    r.upload_scene(s)
+    u = default_uniform(3840, 2160, 0)
+    for (x0, y0, w, h) in [(1904, 1064, 32, 16), (100, 1800, 32, 16), (0, 1080, 1024, 2)]:
+        import torch
+
+        acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        ref = np.zeros((h, w, 4), dtype=np.float32)
+        for f in range(3):
+            e = make_ext(64, 16, 16, frame=f, flags=MM_EXT_ACCUMULATE)
+            r.trace_tile(u, e, x0, y0, w, h, out=acc)
+            o.trace_tile(u, e, x0, y0, w, h, out=ref)
+        got = acc.cpu().numpy()
+        assert np.all(got[..., 3] == 3.0)
+        assert _diff(got, ref) == 0, (x0, y0)
+    r.close()

@@ -83,78 +83,64 @@ def test_parity_mode_accumulates_over_frames(ren):
 
 
 def test_c1_full_frame_matches_fixture_and_oracle(ren, gpu):
-    """C1: 16x16 maze, 256x256, 1 spp, 1 bounce."""
-    from mirror_maze import default_uniform, make_ext
+    """C1: 16x16 maze, 256x256, 1 spp, 1 bounce -- the default query method
+    (grid search) and the lean BVH form, whose work counts are the oracle's."""
+    from mirror_maze import MM_TRAV_AUTO, MM_TRAV_LEAN, default_uniform, make_ext
 
     g = np.load(GOLDEN / "oracle_c1.npz")
     ren.upload_scene(_scene(16))
-    img, st = ren.trace_tile(default_uniform(256, 256, 0), make_ext(1, 1, 15), 0, 0, 256, 256, stats=True)
-    img = img.cpu().numpy()
-    assert np.array_equal(_bits(img[..., :3]), _bits(g["rgb"]))
-    assert st.rays == int(g["rays"]) and st.node_visits == int(g["visits"]) and st.rect_tests == int(g["rtests"])
+    for form in (MM_TRAV_AUTO, MM_TRAV_LEAN):
+        ren.set_option(7, form)
+        img, st = ren.trace_tile(default_uniform(256, 256, 0), make_ext(1, 1, 15), 0, 0, 256, 256, stats=True)
+        img = img.cpu().numpy()
+        assert np.array_equal(_bits(img[..., :3]), _bits(g["rgb"]))
+        assert st.rays == int(g["rays"])
+        if form == MM_TRAV_LEAN:
+            assert st.node_visits == int(g["visits"]) and st.rect_tests == int(g["rtests"])
+    ren.set_option(7, MM_TRAV_AUTO)
 
 
 WINDOWS = [(0, 0), (960, 540), (1888, 1064), (300, 700), (1500, 100)]
 
 
-PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 threshold
-    "reference": (3, {}),
-    "mega-global": (1, {1: 0, 3: 0}),
-    "mega-lds": (1, {1: 1, 3: 0}),
-    "mega-lds-b1024": (1, {1: 1, 2: 1024, 3: 0}),
-    "persist-lds": (1, {1: 1, 3: 1, 8: 0}),
-    "persist-ldsrects": (1, {1: 1, 3: 1, 8: 1}),
-    "persist-global-t0": (1, {1: 0, 3: 1, 4: 0}),
-    "persist-ldsrects-t63-b512-w6": (1, {1: 1, 3: 1, 4: 63, 2: 512, 5: 6}),
-    "persist-lds-t16-b1024-w1": (1, {1: 1, 3: 1, 4: 16, 2: 1024, 5: 1, 8: 0}),
-    "wavepersist-lds": (1, {1: 1, 3: 2, 6: 0, 8: 0, 11: 0}),
-    "wavepersist-ldsrects": (1, {1: 1, 3: 2, 8: 1}),
-    "wavepersist-ldsrects-b512-w6": (1, {1: 1, 3: 2, 8: 1, 2: 512, 5: 6}),
-    "wavepersist-ldsstack": (1, {1: 1, 3: 2, 6: 1, 8: 0}),
-    "wavepersist-ldsstack-b512-w6": (1, {1: 1, 3: 2, 6: 1, 2: 512, 5: 6}),
-    "whilewhile-lds": (1, {1: 1, 3: 2, 7: 1}),
-    "leafbatch16-ldsrects": (1, {1: 1, 3: 2, 7: 16, 8: 1}),
-    "leafbatch8-global": (1, {1: 0, 3: 2, 7: 8}),
-    "whilewhile-global-ldsstack": (1, {1: 0, 3: 2, 7: 1, 6: 1}),
-    "wavepersist-lds-b512-w8": (1, {1: 1, 3: 2, 2: 512, 5: 8}),
-    "wavepersist-split2kb": (1, {1: 1, 3: 2, 9: 2}),
-    "lean-ldsrects": (1, {1: 1, 3: 2, 7: 2, 8: 1}),
-    "lean-ldsstack": (1, {1: 1, 3: 2, 7: 2, 6: 1, 8: 0}),
-    "lean-global-b512-w6": (1, {1: 0, 3: 2, 7: 2, 2: 512, 5: 6}),
-    "lean-split2kb": (1, {1: 1, 3: 2, 7: 2, 9: 2}),
-    "regtop-ldsrects": (1, {1: 1, 3: 2, 7: 3, 8: 1}),
-    "coldlds": (1, {1: 1, 3: 2, 10: 1}),
-    "lds-globalrects": (1, {1: 1, 3: 2, 8: 0, 11: 1}),
-    "split2kb-globalrects": (1, {1: 1, 3: 2, 9: 2, 11: 1}),
-    "split2kb-generalrects": (1, {1: 1, 3: 2, 9: 2, 11: 0}),
-    "bouncerefill-ldsrects": (1, {1: 1, 3: 2, 7: 4, 8: 1}),
-    "bouncerefill-global-b512-w6": (1, {1: 0, 3: 2, 7: 4, 2: 512, 5: 6}),
-    "bouncerefill-split2kb": (1, {1: 1, 3: 2, 7: 4, 9: 2}),
-    "coldlds-b512-w6": (1, {1: 1, 3: 2, 10: 1, 2: 512, 5: 6}),
-    "regtop-split2kb-b512-w6": (1, {1: 1, 3: 2, 7: 3, 9: 2, 2: 512, 5: 6}),
-    "wavepersist-split20kb-b512-w6": (1, {1: 1, 3: 2, 9: 20, 2: 512, 5: 6}),
-    "wavepersist-global-b256": (1, {1: 0, 3: 2, 2: 256}),
-    "leafinterior-ldsrects": (1, {1: 1, 3: 2, 7: 5, 8: 1}),
-    "ifif-ldsrects": (1, {1: 1, 3: 2, 7: 0, 8: 1}),
-    "leafinterior-grab3-fair": (1, {1: 1, 3: 2, 7: 5, 15: 3, 14: 1}),
-    "blocksync": (1, {3: 2, 16: 1}),
-    "leanli": (1, {3: 2, 7: 7}),
-    "leanli-order": (1, {3: 2, 7: 7, 17: 1}),
-    "leanli-dict": (1, {3: 2, 7: 7, 20: 2}),
-    "leafinterior-dict": (1, {3: 2, 7: 5, 20: 2}),
-    "leafinterior-order-grab2": (1, {3: 2, 7: 5, 17: 1, 15: 2}),
-    "cons": (1, {3: 2, 7: 9}),
-    "cons-split2kb": (1, {3: 2, 7: 9, 9: 2}),
-    "cons-globalrects": (1, {3: 2, 7: 9, 8: 0, 11: 1}),
-    "leanli-split2kb": (1, {3: 2, 7: 7, 9: 2}),
-    "blocksync-nofuse": (1, {3: 2, 16: 1, 12: 0}),
-    "leafinterior-lds": (1, {1: 1, 3: 2, 7: 5, 8: 0, 11: 0}),
-    "leafinterior-split2kb": (1, {1: 1, 3: 2, 7: 5, 9: 2}),
-    "leafinterior-global": (1, {1: 0, 3: 2, 7: 5}),
-    "wavepersist-ldsrects-nofuse": (1, {1: 1, 3: 2, 8: 1, 12: 0}),
-    "wavefront": (2, {}),
-    "wavefront-global": (2, {1: 0}),
+# (pipeline, {option: value}, exact_counts); options (include/mm_api.h): 1 LDS,
+# 3 persist, 7 traversal (-1 auto, 0, 5, 7 BVH loop forms, 11 grid search),
+# 8 LDS rect records, 9 split-cache KB, 12 fused resolve, 20 dictionary nodes.
+# exact_counts: node visits and rect tests equal the oracle's (BVH walks); the
+# grid search counts its own work (cells, rect tests), only rays and paths match.
+PIPES = {
+    "reference": (3, {}, True),
+    "mega-global": (1, {1: 0, 3: 0}, True),
+    "mega-lds": (1, {1: 1, 3: 0}, True),
+    "auto": (0, {}, False),                                  # grid search (C3 default)
+    "grid": (1, {7: 11}, False),
+    "grid-nofuse": (1, {7: 11, 12: 0}, False),
+    "bvh-lean-ldsrects": (1, {7: 7}, True),
+    "bvh-lean-globalrecs": (1, {7: 7, 8: 0}, True),
+    "bvh-lean-split2kb": (1, {7: 7, 9: 2}, True),
+    "bvh-lean-dict": (1, {7: 7, 20: 2}, True),
+    "bvh-li-ldsrects": (1, {7: 5}, True),
+    "bvh-li-globalrecs": (1, {7: 5, 8: 0}, True),
+    "bvh-li-global": (1, {7: 5, 1: 0}, True),
+    "bvh-li-split2kb": (1, {7: 5, 9: 2}, True),
+    "bvh-li-dict": (1, {7: 5, 20: 2}, True),
+    "bvh-ifif-ldsrects": (1, {7: 0}, True),
+    "bvh-ifif-lds": (1, {7: 0, 8: 0}, True),
+    "wavefront": (2, {}, True),
+    "wavefront-global": (2, {1: 0}, True),
 }
+
+
+def _renderer(pipe, scene):
+    from mirror_maze import Renderer
+
+    r = Renderer(0)
+    p, opts, _ = PIPES[pipe]
+    r.set_pipeline(p)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload_scene(scene)
+    return r
 
 
 @pytest.mark.parametrize("pipe", sorted(PIPES))
@@ -165,16 +151,11 @@ PIPES = {  # (pipeline, {option: value}); options: 1 lds, 2 block, 3 persist, 4 
     dict(n=32, spp=16, b=8, m=15),  # C4 settings
 ])
 def test_tile_windows_bit_exact(gpu, cfg, pipe):
-    from mirror_maze import Renderer, default_uniform, make_ext
+    from mirror_maze import default_uniform, make_ext
     from oracle.oracle import Oracle
 
     s = _scene(cfg["n"])
-    ren = Renderer(0)
-    p, opts = PIPES[pipe]
-    ren.set_pipeline(p)
-    for k, v in opts.items():
-        ren.set_option(k, v)
-    ren.upload_scene(s)
+    ren = _renderer(pipe, s)
     o = Oracle.from_scene(s)
     u = default_uniform(1920, 1080, 0)
     e = make_ext(cfg["spp"], cfg["b"], cfg["m"], frame=2)
@@ -183,34 +164,24 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
         got, st = ren.trace_tile(u, e, x0, y0, w, h, stats=True)
         ref, rst = o.trace_tile(u, e, x0, y0, w, h)
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
-        if pipe.startswith("cons"):  # the verified search does its own (larger) amount of work
-            assert (st.rays, st.paths) == (rst.rays, rst.paths)
-        else:
-            assert (st.rays, st.node_visits, st.rect_tests, st.paths) == \
-                   (rst.rays, rst.node_visits, rst.rect_tests, rst.paths)
+        assert (st.rays, st.paths) == (rst.rays, rst.paths)
+        if PIPES[pipe][2]:
+            assert (st.node_visits, st.rect_tests) == (rst.node_visits, rst.rect_tests)
     ren.close()
 
 
-@pytest.mark.parametrize("pipe", ["wavepersist-ldsrects", "wavepersist-lds", "mega-global", "leafbatch16-ldsrects",
-                                  "lean-ldsrects", "bouncerefill-ldsrects", "leafinterior-ldsrects",
-                                  "wavepersist-ldsrects-nofuse", "ifif-ldsrects",
-                                  "leafinterior-grab3-fair", "blocksync", "leanli", "cons", "leanli-order",
-                                  "leafinterior-order-grab2", "leanli-dict", "leafinterior-dict"])
+@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "bvh-lean-ldsrects", "bvh-li-dict", "mega-lds",
+                                  "wavefront"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
     cases of the exact-division and threshold tests get exercised."""
-    from mirror_maze import Renderer, default_uniform, make_ext
+    from mirror_maze import default_uniform, make_ext
     from oracle.oracle import Oracle
 
     s = _scene(32)
     o = Oracle.from_scene(s)
-    r = Renderer(0)
-    p, opts = PIPES[pipe]
-    r.set_pipeline(p)
-    for k, v in opts.items():
-        r.set_option(k, v)
-    r.upload_scene(s)
+    r = _renderer(pipe, s)
     u = default_uniform(256, 144, 0)
     for frame in range(3):
         e = make_ext(8, 8, 8, frame=frame)
@@ -244,43 +215,13 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
 
 
-def test_chunk_order_bit_identical(gpu):
-    """MM_OPT_CHUNK_ORDER: chunks handed out longest first (by the previous
-    launch's durations) give the same frames and the same work counts as pixel
-    order -- C3 over several frames, a row-split tile of another geometry in
-    between (the order is keyed on the tile), and an accumulated frame."""
-    import torch
-
-    from mirror_maze import MM_EXT_ACCUMULATE, Renderer, default_uniform, make_ext
-
-    s = _scene(32)
-    base, lpt = Renderer(0), Renderer(0)
-    lpt.set_option(17, 1)
-    for r in (base, lpt):
-        r.upload_scene(s)
-    u = default_uniform(1920, 1080, 0)
-    plan = [(0, 0, 1080, 1), (1, 0, 1080, 1), (2, 0, 1080, 1), (3, 1, 540, 2), (4, 1, 540, 2), (5, 0, 1080, 1),
-            (6, 0, 1080, 1)]
-    for frame, y0, h, stride in plan:
-        e = make_ext(8, 8, 8, frame=frame)
-        a, sa = base.trace_tile(u, e, 0, y0, 1920, h, y_stride=stride, stats=True)
-        b, sb = lpt.trace_tile(u, e, 0, y0, 1920, h, y_stride=stride, stats=True)
-        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), frame
-        assert (sa.rays, sa.node_visits, sa.rect_tests, sa.paths) == (sb.rays, sb.node_visits, sb.rect_tests, sb.paths)
-    e = make_ext(8, 8, 8, frame=7, flags=MM_EXT_ACCUMULATE)
-    base.trace_tile(u, e, 0, 0, 1920, 1080, out=a)
-    lpt.trace_tile(u, e, 0, 0, 1920, 1080, out=b)
-    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
-    base.close()
-    lpt.close()
-
-
-@pytest.mark.parametrize("opts", [{}, {9: 2}, {7: 5, 15: 2, 17: 1}, {19: 8}])
+@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole
-    frames and a row-split tile; the split node cache; loop form 5 with
-    grab 2 and longest-first order; a grid 8 CUs short (MM_OPT_RESERVE_CUS)."""
+    frames and a row-split tile; the grid search (default), the split node
+    cache with loop form 5, the lean BVH form; a grid 8 CUs short
+    (MM_OPT_RESERVE_CUS)."""
     import torch
 
     from mirror_maze import Renderer, default_uniform, make_ext
@@ -389,34 +330,39 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {9: 0}, {9: 8}, {9: 0, 1: 0}, {3: 0}, {11: 0}, {7: 5}, {7: 0}, {7: 7}, {7: 9},
-                                  {20: 1}, {20: 1, 7: 5}],
-                         ids=["auto-split", "split-off", "split-8kb", "global", "mega", "split-generalrects",
-                              "leafinterior", "ifif", "leanli", "cons", "dict", "dict-leafinterior"])
-def test_large_scene_top_of_tree_cache(gpu, opts):
-    """C5's N=64 maze: 5.5 k nodes (177 KB) exceed the LDS budget, so the
-    default kernel caches the top of the breadth-first node array in LDS and
-    reads the rest through L1/L2.  Bit-exact vs the oracle at C5 limits."""
-    from mirror_maze import Renderer, default_uniform, make_ext
+@pytest.mark.parametrize("opts", [{}, {7: 5}, {7: 7}, {7: 5, 20: 0}, {7: 5, 9: 8}, {7: 5, 9: 0},
+                                  {7: 5, 1: 0}, {3: 0}, {7: 11, 1: 0}],
+                         ids=["auto", "li-dict", "lean-dict", "li-split", "li-split-8kb", "li-global-nodes",
+                              "li-nothing-in-lds", "mega", "grid-not-in-lds"])
+def test_large_scene_bit_exact(gpu, opts):
+    """C5's N=64 maze: the grid image (cells, lists, records, leaf boxes) and
+    the BVH (5.5 k nodes, 177 KB) exceed the LDS budget.  Auto runs the grid
+    search with its index in LDS and records / leaf boxes through L1/L2; the
+    BVH forms use dictionary nodes, the top-of-tree cache or global nodes.
+    Bit-exact vs the oracle at C5 limits (16/16 bounces) on 4 windows."""
+    from mirror_maze import MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_GRID_OK, default_uniform, make_ext
     from oracle.oracle import Oracle
 
     s = _scene(64)
     assert s.n_nodes * 32 > 160 * 1024
     o = Oracle.from_scene(s)
+    from mirror_maze import Renderer
+
     r = Renderer(0)
     for k, v in opts.items():
         r.set_option(k, v)
     r.upload_scene(s)
+    assert r.scene_info(MM_INFO_GRID_OK) == 1.0
+    assert r.scene_info(MM_INFO_GRID_BYTES) > 80 * 1024 >= r.scene_info(MM_INFO_GRID_INDEX_BYTES)
     u = default_uniform(3840, 2160, 0)
     e = make_ext(4, 16, 16, frame=5)
     for (x0, y0) in [(0, 0), (1900, 1000), (3000, 1800), (640, 1500)]:
         got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
         ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
-        if opts.get(7) == 9:  # the verified search does its own (larger) amount of work
-            assert st.rays == rst.rays
-        else:
-            assert (st.rays, st.node_visits, st.rect_tests) == (rst.rays, rst.node_visits, rst.rect_tests)
+        assert st.rays == rst.rays
+        if opts.get(7) in (5, 7) or opts.get(3) == 0:
+            assert (st.node_visits, st.rect_tests) == (rst.node_visits, rst.rect_tests)
     r.close()
 
 
