@@ -54,6 +54,8 @@ __device__ __forceinline__ void grid_rect(const R& recs, uint32_t k, const Ray& 
     const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
     const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
     const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
+    // (a branch-free update measured 6.11 vs 5.86 ms on C3: most tests miss,
+    // and the branch skips the update for the whole wave)
     if (x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) && x2 >= __uint_as_float(w67.y) &&
         x2 <= __uint_as_float(w89.x) && a > 0.1f) {
         if (a < best) {
@@ -89,9 +91,17 @@ __device__ __forceinline__ int grid_cell(const DevGrid& g, float o, int a) {
     return min(max(i, 0), g.n[a] - 1);
 }
 
-// The next boundary crossing on axis a from cell i: (boundary - o) * (1/d).
-__device__ __forceinline__ float grid_next(const DevGrid& g, int a, int i, bool up, float o, float y) {
-    return ((g.mn[a] + (float)(i + (up ? 1 : 0)) * g.cell[a]) - o) * y;
+// DDA state per axis: the index b of the next cell boundary the ray crosses
+// (boundary b lies at mn + b * cell) and the time it crosses it; the step
+// direction is the sign of y = 1/d.  Going up, the current cell is b - 1
+// and the walk leaves the grid past boundary n; going down, the cell is b
+// and it leaves below boundary 0.
+__device__ __forceinline__ float grid_time(const DevGrid& g, int a, int b, float o, float y) {
+    return ((g.mn[a] + (float)b * g.cell[a]) - o) * y;
+}
+__device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, float y) {
+    const int i = min(max((int)floorf((o - g.mn[a]) * g.inv[a]), 0), g.n[a] - 1);
+    return y > 0.0f ? i + 1 : i;
 }
 
 // Search + certificate.  Returns true with (t, index) = the reference's answer
@@ -104,12 +114,14 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     uint32_t bk = 0xFFFFFFFFu;
     bool tie = false;
     for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect(gv.recs, g.glob[j], r, best, bk, tie);
-    const bool ux = r.d.x > 0.0f, uy = r.d.y > 0.0f, uz = r.d.z > 0.0f;
-    int ix = grid_cell(g, r.o.x, 0), iy = grid_cell(g, r.o.y, 1), iz = grid_cell(g, r.o.z, 2);
-    float tx = grid_next(g, 0, ix, ux, r.o.x, r.y.x);
-    float ty = grid_next(g, 1, iy, uy, r.o.y, r.y.y);
-    float tz = grid_next(g, 2, iz, uz, r.o.z, r.y.z);
-    uint32_t cw = gv.cells[(iz * g.n[1] + iy) * g.n[0] + ix];
+    int bx = grid_first(g, 0, r.o.x, r.y.x), by = grid_first(g, 1, r.o.y, r.y.y), bz = grid_first(g, 2, r.o.z, r.y.z);
+    float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
+          tz = grid_time(g, 2, bz, r.o.z, r.y.z);
+    auto cell_word = [&]() {
+        const int ix = r.y.x > 0.0f ? bx - 1 : bx, iy = r.y.y > 0.0f ? by - 1 : by, iz = r.y.z > 0.0f ? bz - 1 : bz;
+        return gv.cells[(iz * g.n[1] + iy) * g.n[0] + ix];
+    };
+    uint32_t cw = cell_word();
     uint32_t j = cw & 0x3FFFFFu, jend = j + (cw >> 22);
     uint32_t cells = 1, tests = g.n_glob;
     // One iteration: test one rect of the current cell; when the cell's list
@@ -124,19 +136,19 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             const float te = fminf(tx, fminf(ty, tz));
             if (best < te) break;
             if (tx == te) {
-                ix += ux ? 1 : -1;
-                if (ix < 0 || ix >= g.n[0]) break;
-                tx = grid_next(g, 0, ix, ux, r.o.x, r.y.x);
+                bx += r.y.x > 0.0f ? 1 : -1;
+                if (bx < 0 || bx > g.n[0]) break;
+                tx = grid_time(g, 0, bx, r.o.x, r.y.x);
             } else if (ty == te) {
-                iy += uy ? 1 : -1;
-                if (iy < 0 || iy >= g.n[1]) break;
-                ty = grid_next(g, 1, iy, uy, r.o.y, r.y.y);
+                by += r.y.y > 0.0f ? 1 : -1;
+                if (by < 0 || by > g.n[1]) break;
+                ty = grid_time(g, 1, by, r.o.y, r.y.y);
             } else {
-                iz += uz ? 1 : -1;
-                if (iz < 0 || iz >= g.n[2]) break;
-                tz = grid_next(g, 2, iz, uz, r.o.z, r.y.z);
+                bz += r.y.z > 0.0f ? 1 : -1;
+                if (bz < 0 || bz > g.n[2]) break;
+                tz = grid_time(g, 2, bz, r.o.z, r.y.z);
             }
-            cw = gv.cells[(iz * g.n[1] + iy) * g.n[0] + ix];
+            cw = cell_word();
             j = cw & 0x3FFFFFu;
             jend = j + (cw >> 22);
             if (kStats) ++cells;
@@ -152,13 +164,13 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     }
     if (tie) return false;
     // certificate: R*'s reference leaf box passes at every t > best
-    const float2 bx = gv.box[3 * bk + 0], by = gv.box[3 * bk + 1], bz = gv.box[3 * bk + 2];
-    const float tx1 = qdiv(bx.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(bx.y - r.o.x, r.d.x, r.y.x);
+    const float2 bxx = gv.box[3 * bk + 0], byy = gv.box[3 * bk + 1], bzz = gv.box[3 * bk + 2];
+    const float tx1 = qdiv(bxx.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(bxx.y - r.o.x, r.d.x, r.y.x);
     float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
-    const float ty1 = qdiv(by.x - r.o.y, r.d.y, r.y.y), ty2 = qdiv(by.y - r.o.y, r.d.y, r.y.y);
+    const float ty1 = qdiv(byy.x - r.o.y, r.d.y, r.y.y), ty2 = qdiv(byy.y - r.o.y, r.d.y, r.y.y);
     tmin = fmaxf(tmin, fminf(ty1, ty2));
     tmax = fminf(tmax, fmaxf(ty1, ty2));
-    const float tz1 = qdiv(bz.x - r.o.z, r.d.z, r.y.z), tz2 = qdiv(bz.y - r.o.z, r.d.z, r.y.z);
+    const float tz1 = qdiv(bzz.x - r.o.z, r.d.z, r.y.z), tz2 = qdiv(bzz.y - r.o.z, r.d.z, r.y.z);
     tmin = fmaxf(tmin, fminf(tz1, tz2));
     tmax = fminf(tmax, fmaxf(tz1, tz2));
     if (!(tmax >= tmin && tmax > 0.0f && tmin <= best)) return false;

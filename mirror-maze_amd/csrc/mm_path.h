@@ -40,7 +40,7 @@ struct GridQuery {
         const Ray r = make_ray(o, d);
         if (sc.fast_ok && ray_fast_ok(r) && grid_ray_ok(sc.grid, r) && grid_search<kStats>(sc.grid, gv, r, t, k, c))
             return true;
-        t = kBig;
+        t = kBig;  // (an out-of-line walk costs 73 VGPR spills of call ABI)
         return closest_hit_bvh<kStats, kFormLean>(sc, view(sc.nodes, sc.recs), r, t, k, st, c);
     }
 };

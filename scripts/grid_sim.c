@@ -97,11 +97,12 @@ static void build_grid(double cell_target) {
     for (int a = 0; a < 3; ++a) {
         double lo = smin[a] - geps, hi = smax[a] + geps;
         int n = (int)floor((hi - lo) / cell_target + 0.5);
+        if (getenv("ALIGN")) n = (int)ceil((hi - lo) / cell_target);
         if (n < 1) n = 1;
         if (n > 256) n = 256;
         gn[a] = n;
         gmin[a] = (float)lo;
-        gcell[a] = (float)((hi - lo) / n);
+        gcell[a] = getenv("ALIGN") ? (float)cell_target : (float)((hi - lo) / n);
         ginv[a] = 1.0f / gcell[a];
         total *= n;
     }
@@ -175,6 +176,9 @@ static inline void consider(float a, uint32_t k, float* best, uint32_t* bk, int*
 }
 
 /* grid search + verification; returns 1 and (t, index) when certified */
+#define MAXC 128
+static __thread int q_len[MAXC];   /* list lengths of the cells the last query visited */
+static __thread int q_n;
 static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
     float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, yy[3];
     for (int a = 0; a < 3; ++a) {
@@ -198,9 +202,12 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
         tn[a] = (gmin[a] + (float)(i + (stp[a] > 0)) * gcell[a] - oo[a]) * yy[a];
     }
     int ncell = 0;
+    q_n = 0;
     for (;;) {
         long c = ((long)ic[2] * gn[1] + ic[1]) * gn[0] + ic[0];
+        if (ncell < MAXC) q_len[ncell] = (int)(cell_off[c + 1] - cell_off[c]);
         ncell++;
+        q_n = ncell < MAXC ? ncell : MAXC;
         for (uint32_t j = cell_off[c]; j < cell_off[c + 1]; ++j) {
             uint32_t k = cell_list[j];
             consider(rect_a(o, d, &S.rects[k]), k, &best, &bk, &tie);
@@ -232,6 +239,9 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
     return 1;
 }
 
+/* wave model: per lane, per bounce, the list lengths of the visited cells */
+#define MAXB 32
+static __thread int w_len[64][MAXB][16], w_n[64][MAXB], w_nb[64], w_lane;
 /* the reference path loop with every query cross-checked */
 static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t* tr, uint64_t* rays) {
     ray_t b;
@@ -243,7 +253,13 @@ static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t
         (*rays)++;
         float gt; uint32_t gi;
         st->queries++;
-        if (grid_query(b.ori, b.dir, &gt, &gi, st)) {
+        int ok_q = grid_query(b.ori, b.dir, &gt, &gi, st);
+        if (n < MAXB) {
+            w_n[w_lane][n] = q_n < 16 ? q_n : 16;
+            for (int c = 0; c < w_n[w_lane][n]; ++c) w_len[w_lane][n][c] = q_len[c];
+            w_nb[w_lane] = n + 1;
+        }
+        if (ok_q) {
             if (gt != b.t || (gt < BIG && gi != b.index)) {
                 st->mismatch++;
                 if (st->mismatch < 10)
@@ -305,6 +321,7 @@ int main(int argc, char** argv) {
     u.view_w = (float)W; u.view_h = (float)H; u.chunk_w = 4; u.time = 0;
     gstats tot;
     memset(&tot, 0, sizeof tot);
+    double wnest = 0, wflat = 0, wlane = 0, wcont[4] = {0, 0, 0, 0};
     uint64_t rays_tot = 0;
 #pragma omp parallel
     {
@@ -312,16 +329,69 @@ int main(int argc, char** argv) {
         memset(&st, 0, sizeof st);
         trav_t tr = {0, 0, 0};
         uint64_t rays = 0;
+        double nest = 0, flat = 0, lanework = 0, ideal = 0, lockS = 0, cont[4] = {0, 0, 0, 0};
 #pragma omp for schedule(dynamic, 1)
         for (int y = 0; y < H; y += rs)
-            for (int x = 0; x < W; ++x) {
-                v3 d0 = primary_dir(&u, x, y);
-                for (int k = 0; k < spp; ++k) {
+            for (int x0 = 0; x0 < W; x0 += 64 / spp) {
+                for (int l = 0; l < 64; ++l) {
+                    int x = x0 + l / spp, k = l % spp;
+                    w_lane = l; w_nb[l] = 0;
+                    if (x >= W) continue;
+                    v3 d0 = primary_dir(&u, x, y);
                     uint32_t seed = oracle_tile_seed(y * W + x, k, 0);
                     v3 d = jittered_dir(d0, &seed);
                     path(ld3(u.cam.center), d, seed, bl, ml, &st, &tr, &rays);
                 }
+                /* per bounce: nested (inner list loop per cell step) vs flat (one test or step per iteration) */
+                for (int b = 0; b < MAXB; ++b) {
+                    int any = 0, maxc = 0, maxflat = 0;
+                    for (int l = 0; l < 64; ++l) if (w_nb[l] > b) {
+                        any = 1;
+                        int nc = w_n[l][b], fl = 0;
+                        if (nc > maxc) maxc = nc;
+                        for (int c = 0; c < nc; ++c) { fl += w_len[l][b][c] > 0 ? w_len[l][b][c] : 1; lanework += w_len[l][b][c] * 45.0 + 25.0; }
+                        if (fl > maxflat) maxflat = fl;
+                    }
+                    if (!any) break;
+                    for (int c = 0; c < maxc; ++c) {
+                        int mx = 0;
+                        for (int l = 0; l < 64; ++l) if (w_nb[l] > b && w_n[l][b] > c && w_len[l][b][c] > mx) mx = w_len[l][b][c];
+                        nest += mx * 45.0 + 25.0;
+                    }
+                    flat += maxflat * 70.0;
+                    lockS += 250.0;
+                }
+                /* continuous (lanes run their bounces back to back) with batched shading */
+                for (int K = 0; K < 4; ++K) {
+                    int thr = (int[]){1, 16, 32, 64}[K];
+                    int bi[64], rem[64], state[64];   /* state 0 querying, 1 waiting for shade, 2 done */
+                    for (int l = 0; l < 64; ++l) {
+                        bi[l] = 0; state[l] = w_nb[l] > 0 ? 0 : 2; rem[l] = 0;
+                        if (state[l] == 0) { int fl = 0; for (int c = 0; c < w_n[l][0]; ++c) fl += w_len[l][0][c] > 0 ? w_len[l][0][c] : 1; rem[l] = fl; }
+                    }
+                    double cost = 250.0; /* first setup */
+                    for (;;) {
+                        int nq = 0, nw = 0;
+                        for (int l = 0; l < 64; ++l) { nq += state[l] == 0; nw += state[l] == 1; }
+                        if (nq == 0 && nw == 0) break;
+                        if (nw >= thr || (nq == 0 && nw > 0)) {
+                            cost += 250.0;
+                            for (int l = 0; l < 64; ++l) if (state[l] == 1) {
+                                bi[l]++;
+                                if (bi[l] >= w_nb[l] || bi[l] >= MAXB) { state[l] = 2; continue; }
+                                int fl = 0; for (int c = 0; c < w_n[l][bi[l]]; ++c) fl += w_len[l][bi[l]][c] > 0 ? w_len[l][bi[l]][c] : 1;
+                                rem[l] = fl; state[l] = 0;
+                            }
+                            continue;
+                        }
+                        cost += 70.0;
+                        for (int l = 0; l < 64; ++l) if (state[l] == 0 && --rem[l] <= 0) state[l] = 1;
+                    }
+                    cont[K] += cost;
+                }
             }
+#pragma omp critical
+        { wnest += nest + lockS; wflat += flat + lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K]; }
 #pragma omp critical
         {
             tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
@@ -336,6 +406,10 @@ int main(int argc, char** argv) {
            (unsigned long long)tot.queries, tot.cells / q, tot.tests / q, 100 * tot.fallback_tie / q,
            100 * tot.fallback_verify / q, 100 * tot.fallback_guard / q, (unsigned long long)tot.miss,
            (unsigned long long)tot.mismatch);
+    printf("wave model (VALU slots x64 per wave): nested %.4g  flat %.4g  ideal(lane work/64) %.4g  -> util nested %.3f flat %.3f\n",
+           wnest, wflat, wlane / 64, wlane / 64 / wnest, wlane / 64 / wflat);
+    printf("with shading (250/bounce): lockstep nested %.4g flat %.4g | continuous thr1 %.4g thr16 %.4g thr32 %.4g thr64 %.4g\n",
+           wnest, wflat, wcont[0], wcont[1], wcont[2], wcont[3]);
     printf("cells hist:");
     for (int i = 1; i < 40; ++i) printf(" %d:%.3f", i, tot.hist_cells[i] / q);
     printf("\n");
