@@ -42,9 +42,44 @@ CONFIGS = {
     "c5s": (64, 1920, 1080, 8, 16, 16, "C5 scene at C3 size: 64x64 maze, 1920x1080, 8 spp, 16/16 bounces"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, non-packed fp32 ops
+VALU_PEAK_TOPS = 78.6          # 256 CU x 4 SIMD x 32 lanes/cycle x 2.4 GHz, non-packed fp32 lane-ops
 BYTES_PER_RAY = 136            # SoA path state read+write + hit record
 BYTES_PER_PIXEL = 16           # float4 output
+OPS_PER_AABB, OPS_PER_RECT = 25, 71  # SURVEY.md §8(d) VALU model of the reference BVH walk
+SRC_GLOBS = ("mirror-maze_amd/csrc/*", "mirror-maze_amd/Makefile", "include/*.h")
+
+
+def src_hash() -> str:
+    """sha256 (16 hex) of the product sources the trace kernels are built from;
+    a PMC profile under profiles/ is used only when it carries the same hash."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for pat in SRC_GLOBS:
+        for f in sorted(REPO.glob(pat)):
+            if f.is_file():
+                h.update(str(f.relative_to(REPO)).encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def usable_cpus():
+    """CPUs this process may run on: its affinity set, capped by the cgroup's
+    cpu.max quota (a GPU box gives each GPU a share of its host's CPUs).
+    Returns (count, basis)."""
+    import math
+
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n, basis = aff, f"sched_getaffinity {aff} of {os.cpu_count()} online CPUs"
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            q = max(1, math.ceil(int(quota) / int(period)))
+            if q < n:
+                n = q
+                basis += f", cgroup cpu.max quota {quota}/{period} = {q} CPUs"
+    except (OSError, ValueError):
+        pass
+    return n, basis
 
 
 def parse():
@@ -71,6 +106,7 @@ def parse():
                    help="mm_set_option on every context (MM_OPT_* numbers, include/mm_api.h); results never change")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (approx)")
+    p.add_argument("--src-hash", action="store_true", help="print the product source hash and exit")
     return p.parse_args()
 
 
@@ -93,7 +129,7 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
     from oracle.oracle import Oracle
 
     o = Oracle.from_scene(scene)
-    threads = max(1, min(16, (os.cpu_count() or 1)))
+    threads, basis = usable_cpus()
     # calibrate on one row, then pick a row sample that fits the budget
     t0 = time.perf_counter()
     _, st = o.trace_tile(u, ext, 0, H // 2, W, 1)
@@ -130,7 +166,8 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
         _, s1 = o.trace_tile(u, ext, 0, y, W, 1)
         rays1 += s1.rays
     dt1 = time.perf_counter() - t0
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "cores_basis": basis,
+            "kind": "port",
             "sample": f"{len(sample_rows)} of {H} rows (every {stride}th) x {W} px x {ext.spp} spp, "
                       f"{rays} rays in {dt:.1f} s; scalar C oracle -O2 -ffp-contract=off",
             "single_core": {"value": round(rays1 / dt1 / 1e6, 3), "unit": "Mrays/s",
@@ -138,8 +175,39 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
             "host_cpus": os.cpu_count()}
 
 
+def pmc_profile(args, frames_per_launch, k_avg_s, world):
+    """Measured counters of the dominant kernel from profiles/pmc_<config>.json
+    (scripts/pmc_record.py over rocprofv3 --pmc passes of `bench.py --steps 5
+    --warmup 0`), used only when its source hash is this tree's.  Returns
+    (measured dict, HBM bytes per launch or None)."""
+    f = REPO / "profiles" / f"pmc_{args.config}.json"
+    if not f.exists() or args.pipeline != "auto" or args.opt or args.emulate_ranks or world > 1:
+        return {"source": None, "note": "no PMC profile for this configuration"}, None
+    rec = json.loads(f.read_text())
+    here = src_hash()
+    if rec.get("src_hash") != here:
+        return {"source": str(f.relative_to(REPO)), "stale": True, "profile_src_hash": rec.get("src_hash"),
+                "src_hash": here, "note": "profile of other kernel sources: not used"}, None
+    scale = frames_per_launch / rec["frames_per_launch"]
+    hbm = rec["hbm_bytes_per_launch"] * scale
+    m = {"source": str(f.relative_to(REPO)), "src_hash": here, "git_head": rec.get("git_head"),
+         "hbm_bytes_per_launch": round(hbm), "hbm_gbs": round(hbm / k_avg_s / 1e9, 1),
+         "hbm_frac": round(hbm / k_avg_s / 1e9 / HBM_PEAK_GBS, 5),
+         "valu_issue_share": rec.get("valu_issue_share"), "lane_utilisation": rec.get("lane_utilisation"),
+         "valu_lane_ops_tops": (round(rec["valu_lane_ops_per_launch"] * scale / k_avg_s / 1e12, 3)
+                                if rec.get("valu_lane_ops_per_launch") else None),
+         "profile_kernel_avg_ms": rec.get("kernel_avg_ms"),
+         "note": ("rocprofv3 --pmc passes: HBM = 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE; lane "
+                  "utilisation = SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU); issue share = SQ_INSTS_VALU / "
+                  "(1024 SIMDs x cycles / 2); per launch, scaled to this run's frames per launch")}
+    return m, round(hbm)
+
+
 def main():
     args = parse()
+    if args.src_hash:
+        print(src_hash())
+        return
     # Exactly one JSON line on stdout: anything else written to fd 1 (e.g. the
     # RCCL banner at communicator init) is sent to stderr.
     json_out = os.fdopen(os.dup(1), "w")
@@ -349,13 +417,30 @@ def main():
         k_ms += ms
         k_launches += n
 
-    # count the rays of exactly the timed frames (deterministic re-run, untimed)
-    rays = paths = visits = rtests = 0
+    # count the rays of exactly the timed frames (deterministic re-run, untimed), and the reference BVH
+    # walk's work on the same frames (node visits = 2 AABB tests each, rect tests) with the BVH loop form,
+    # whose counts equal the oracle's (tests/test_gpu_parity.py) -- the SURVEY 8(d) VALU model's inputs
+    rays = paths = 0
     for i in range(args.steps):
         st = step(i, i, stats=True)
-        rays += st.rays; paths += st.paths; visits += st.node_visits; rtests += st.rect_tests
+        rays += st.rays; paths += st.paths
         progress(f"counting rays: frame {i + 1}/{args.steps}")
     drain()
+    from mirror_maze import MM_INFO_LEAN, MM_TRAV_LEAF_INTERIOR, MM_TRAV_LEAN
+    counter = Renderer(local)
+    counter.upload_scene(scene)
+    counter.set_option(7, MM_TRAV_LEAN if counter.scene_info(MM_INFO_LEAN) else MM_TRAV_LEAF_INTERIOR)
+    visits = rtests = ref_rays = 0
+    cnt_out = torch.empty((my_rows, W, 4), dtype=torch.float32, device=dev)
+    with torch.cuda.stream(counter.own_stream()):
+        for i in range(args.steps):
+            _, st = counter.trace_tile(u, make_ext(spp, bl, ml, frame=i), 0, y0, W, my_rows, y_stride=y_stride,
+                                       out=cnt_out, stats=True)
+            visits += st.node_visits; rtests += st.rect_tests; ref_rays += st.rays
+            progress(f"counting reference work: frame {i + 1}/{args.steps}")
+    torch.cuda.synchronize(dev)
+    counter.close()
+    assert ref_rays == rays or args.accumulate, (ref_rays, rays)
     counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
     t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if distributed:
@@ -370,17 +455,11 @@ def main():
         value = rays_all / elapsed / 1e6
         # roofline of the dominant kernel (ray trace), rank 0's launches
         k_avg_s = (k_ms / 1e3) / max(k_launches, 1)
-        rays_per_launch = rays / max(k_launches, 1)            # rank-0 rays over its launches
-        pix_per_launch = (my_rows * W * args.steps) / max(k_launches, 1)
-        alg_bytes = BYTES_PER_RAY * rays_per_launch + BYTES_PER_PIXEL * pix_per_launch
-        achieved = alg_bytes / k_avg_s / 1e9
-        traffic = None
-        tf = REPO / "profiles" / f"traffic_{args.config}_{args.pipeline}.json"
-        if tf.exists() and not args.emulate_ranks:  # measured on whole-frame launches: per frame x frames/launch
-            rec = json.loads(tf.read_text())
-            t1 = rec.get("hbm_bytes_per_frame", rec.get("hbm_bytes_per_launch"))
-            traffic = None if t1 is None or world > 1 else round(t1 * args.steps / max(k_launches, 1))
-        valu_ops = (25 * 2 * (visits / max(k_launches, 1)) + 71 * (rtests / max(k_launches, 1)))
+        per_launch = 1.0 / max(k_launches, 1)
+        ops = (OPS_PER_AABB * 2 * visits + OPS_PER_RECT * rtests) * per_launch   # reference-walk VALU model
+        alg_bytes = (BYTES_PER_RAY * rays + BYTES_PER_PIXEL * my_rows * W * args.steps) * per_launch
+        frames_per_launch = args.steps * per_launch
+        measured, traffic = pmc_profile(args, frames_per_launch, k_avg_s, world)
         line = {
             "metric": "Mrays/sec + ms/frame at 1920x1080, 8 spp, 8 bounces; 1/2/4/8-GPU scaling",
             "value": round(value, 2),
@@ -408,16 +487,23 @@ def main():
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),
                        "node_visits_per_ray": round(visits_all / max(rays_all, 1), 2),
                        "rect_tests_per_ray": round(rtests_all / max(rays_all, 1), 2)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "trace", "kernel_avg_ms": round(k_avg_s * 1e3, 3), "launches": k_launches,
+            "roofline": {"bound": "valu", "achieved": round(ops / k_avg_s / 1e12, 3), "peak": VALU_PEAK_TOPS,
+                         "unit": "TFLOP/s", "frac": round(ops / k_avg_s / 1e12 / VALU_PEAK_TOPS, 4),
+                         "traffic": traffic,
+                         "ops": ("fp32 VALU lane-ops of the reference BVH walk on the timed frames (SURVEY 8d "
+                                 "model: 25 per AABB test + 71 per rect test, counted by the BVH loop form) "
+                                 "per launch / mean launch time; peak = 256 CU x 128 lanes/clk x 2.4 GHz"),
+                         "kernel": "k_trace_wavepersist", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
+                         "launches": k_launches, "frames_per_launch": round(frames_per_launch, 3),
                          "timing": ("HIP events around each launch on its stream" +
                                     ("; 2 contexts: consecutive launches overlap, so a launch's "
                                      "span includes time shared with its neighbours" if active[0] > 1 else "")),
-                         "bytes_per_ray": BYTES_PER_RAY,
-                         "valu": {"achieved_tops": round(valu_ops / k_avg_s / 1e12, 3), "peak_tops": VALU_PEAK_TOPS,
-                                  "frac": round(valu_ops / k_avg_s / 1e12 / VALU_PEAK_TOPS, 4),
-                                  "ops": "25 per AABB test + 71 per rect test (SURVEY 8d)"}},
+                         "model_hbm": {"bytes_per_ray": BYTES_PER_RAY, "bytes_per_launch": round(alg_bytes),
+                                       "achieved_gbs": round(alg_bytes / k_avg_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+                                       "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                                       "note": ("SURVEY 8(d) accounting model of a SoA wavefront (136 B/ray + 16 "
+                                                "B/px), not traffic: the megakernel keeps path state in registers")},
+                         "measured": measured},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

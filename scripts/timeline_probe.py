@@ -28,9 +28,6 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=3)
-    ap.add_argument("--fair", default="0", help="comma list of MM_OPT_FAIR values to compare")
-    ap.add_argument("--grab", type=int, default=1)
-    ap.add_argument("--order", type=int, default=0, help="MM_OPT_CHUNK_ORDER")
     a = ap.parse_args()
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
     r = Renderer(0)
@@ -38,10 +35,7 @@ def main():
     u = default_uniform(W, H, 0)
     ts = torch.zeros((65536, 4), dtype=torch.int64, device="cuda")
     print(f"# {desc}; times in us (wall_clock64, 100 MHz)")
-    for fair, n in [(int(f), int(x)) for f in a.fair.split(",") for x in a.ranks.split(",")]:
-        r.set_option(14, fair)
-        r.set_option(15, a.grab)
-        r.set_option(17, a.order)
+    for n in [int(x) for x in a.ranks.split(",")]:
         y0, stride, rows = row_shard(H, n, 0)
         out = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda")
         r.trace_tile(u, make_ext(spp, bl, ml, frame=99), 0, y0, W, rows, y_stride=stride, out=out)
@@ -57,7 +51,7 @@ def main():
             ent, stg, ext, ch = ((t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0, t[:, 3])
             span = ext.max()
             busy = (ext - np.maximum(stg, ent)).sum()
-            print(f"fair={fair} order={a.order} N={n} f{f}: waves {len(t)} span {span:8.1f}  entry p50/max {np.median(ent):6.1f}/{ent.max():6.1f}  "
+            print(f"N={n} f{f}: waves {len(t)} span {span:8.1f}  entry p50/max {np.median(ent):6.1f}/{ent.max():6.1f}  "
                   f"staged p50/max {np.median(stg):6.1f}/{stg.max():6.1f}  exit min/p10/p50/p90/max "
                   f"{ext.min():7.1f}/{np.percentile(ext, 10):7.1f}/{np.median(ext):7.1f}/{np.percentile(ext, 90):7.1f}/"
                   f"{ext.max():7.1f}  tail {span - ext.min():6.1f} ({(span - ext.min()) / span:.1%})  "

@@ -382,7 +382,8 @@ def test_bench_prints_one_json_line(gpu):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["unit"] == "Mrays/s" and d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2
-    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    assert d["roofline"]["bound"] == "valu" and 0 < d["roofline"]["frac"] < 1
+    assert d["roofline"]["model_hbm"]["bytes_per_ray"] == 136 and "measured" in d["roofline"]
     assert d["config"]["frame_contexts"] in (1, 2)
     assert d["config"]["frames_per_launch"] == 2  # default batching: the 2 timed frames in one launch
     assert d["roofline"]["launches"] == 1
