@@ -179,7 +179,10 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
  *   MM_INFO_GRID_BYTES       the grid image (cells, lists, records, leaf boxes)
  *   MM_INFO_GRID_INDEX_BYTES its cells + lists part
  *   MM_INFO_LEAN             1 if every rect has a compact record
- *   MM_INFO_DEPTH            BVH depth (max traversal stack entries) */
+ *   MM_INFO_DEPTH            BVH depth (max traversal stack entries)
+ *   MM_INFO_DICT_OK          1 if the nodes have <= 256 distinct bound values (dictionary nodes possible)
+ *   MM_INFO_LAST_FORM        query method of the last wave-persistent launch (MM_OPT_TRAVERSAL value)
+ *   MM_INFO_LAST_LDS_MODE    its LDS mode (trace_kernels.hip: 0, 1, 3, 6, 7, 10 BVH; 11-13 grid) */
 #define MM_INFO_GRID_OK          1
 #define MM_INFO_GRID_CELLS_X     2
 #define MM_INFO_GRID_CELLS_Y     3
@@ -189,6 +192,9 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
 #define MM_INFO_GRID_INDEX_BYTES 7
 #define MM_INFO_LEAN             8
 #define MM_INFO_DEPTH            9
+#define MM_INFO_DICT_OK          10
+#define MM_INFO_LAST_FORM        11
+#define MM_INFO_LAST_LDS_MODE    12
 int  mm_scene_info(const mm_ctx* ctx, int key, double* value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

@@ -96,6 +96,7 @@ struct mm_ctx {
     bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
+    int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
     // per-kernel profiling of the trace kernel (mm_set_profiling)
@@ -384,6 +385,9 @@ int mm_scene_info(const mm_ctx* c, int key, double* value) {
         case MM_INFO_GRID_INDEX_BYTES: *value = g.off_recs; return MM_OK;
         case MM_INFO_LEAN: *value = c->lean_ok ? 1.0 : 0.0; return MM_OK;
         case MM_INFO_DEPTH: *value = c->depth; return MM_OK;
+        case MM_INFO_DICT_OK: *value = c->dict_ok ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_LAST_FORM: *value = c->last_form; return MM_OK;
+        case MM_INFO_LAST_LDS_MODE: *value = c->last_mode; return MM_OK;
         default: return MM_ERR_INVALID;
     }
 }
@@ -784,6 +788,8 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             int form = 0, mode = 0;
             DevScene sc = dev_scene(c);
             if ((rc = choose_wavepersist(c, sc, form, mode))) return rc;
+            c->last_form = form;
+            c->last_mode = mode;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,

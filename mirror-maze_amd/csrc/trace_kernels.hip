@@ -213,6 +213,9 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     } while (0)
 
 template <bool kStats, int kLds, int kForm>
+// 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
+// 768-thread blocks at 6 waves (80 VGPRs, no VGPR spills) measured 6.21 vs
+// 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).
 __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {

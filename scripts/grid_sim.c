@@ -117,8 +117,9 @@ static void build_grid(double cell_target) {
             int i0[3], i1[3];
             long cover = 1;
             for (int a = 0; a < 3; ++a) {
-                i0[a] = (int)floor((lo[a] - geps - gmin[a]) / gcell[a]);
-                i1[a] = (int)floor((hi[a] + geps - gmin[a]) / gcell[a]);
+                double le = getenv("NOEPS") ? 0.0 : geps;
+                i0[a] = (int)floor((lo[a] - le - gmin[a]) / gcell[a]);
+                i1[a] = (int)floor((hi[a] + le - gmin[a]) / gcell[a]);
                 if (i0[a] < 0) i0[a] = 0;
                 if (i1[a] > gn[a] - 1) i1[a] = gn[a] - 1;
                 cover *= (i1[a] - i0[a] + 1);
@@ -322,6 +323,7 @@ int main(int argc, char** argv) {
     gstats tot;
     memset(&tot, 0, sizeof tot);
     double wnest = 0, wflat = 0, wlane = 0, wcont[4] = {0, 0, 0, 0};
+    double gnbmax = 0, gnbsum = 0, gnbw = 0, gact[32] = {0}, git[32] = {0};
     uint64_t rays_tot = 0;
 #pragma omp parallel
     {
@@ -330,6 +332,7 @@ int main(int argc, char** argv) {
         trav_t tr = {0, 0, 0};
         uint64_t rays = 0;
         double nest = 0, flat = 0, lanework = 0, ideal = 0, lockS = 0, cont[4] = {0, 0, 0, 0};
+        double nbmax = 0, nbsum = 0, nbw = 0, act_hist[32] = {0}, it_hist[32] = {0};
 #pragma omp for schedule(dynamic, 1)
         for (int y = 0; y < H; y += rs)
             for (int x0 = 0; x0 < W; x0 += 64 / spp) {
@@ -342,6 +345,11 @@ int main(int argc, char** argv) {
                     v3 d = jittered_dir(d0, &seed);
                     path(ld3(u.cam.center), d, seed, bl, ml, &st, &tr, &rays);
                 }
+                { int mx = 0, sum = 0, cnt = 0;
+                  for (int l = 0; l < 64; ++l) if (w_nb[l] > 0) { sum += w_nb[l]; cnt++; if (w_nb[l] > mx) mx = w_nb[l]; }
+                  if (cnt) { nbmax += mx; nbsum += (double)sum / cnt; nbw++;
+                    /* lanes still active at bounce b, summed: lane-iterations in bounces >= 8 with <= 16 lanes */
+                    for (int b = 0; b < mx; ++b) { int act = 0; for (int l = 0; l < 64; ++l) act += w_nb[l] > b; act_hist[b < 31 ? b : 31] += act; it_hist[b < 31 ? b : 31] += 1; } } }
                 /* per bounce: nested (inner list loop per cell step) vs flat (one test or step per iteration) */
                 for (int b = 0; b < MAXB; ++b) {
                     int any = 0, maxc = 0, maxflat = 0;
@@ -391,7 +399,8 @@ int main(int argc, char** argv) {
                 }
             }
 #pragma omp critical
-        { wnest += nest + lockS; wflat += flat + lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K]; }
+        { wnest += nest + lockS; wflat += flat + lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K];
+          gnbmax += nbmax; gnbsum += nbsum; gnbw += nbw; for (int b = 0; b < 32; ++b) { gact[b] += act_hist[b]; git[b] += it_hist[b]; } }
 #pragma omp critical
         {
             tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
@@ -410,6 +419,10 @@ int main(int argc, char** argv) {
            wnest, wflat, wlane / 64, wlane / 64 / wnest, wlane / 64 / wflat);
     printf("with shading (250/bounce): lockstep nested %.4g flat %.4g | continuous thr1 %.4g thr16 %.4g thr32 %.4g thr64 %.4g\n",
            wnest, wflat, wcont[0], wcont[1], wcont[2], wcont[3]);
+    printf("per wave: mean of max queries/lane %.3f, mean queries/lane %.3f\n", gnbmax / gnbw, gnbsum / gnbw);
+    printf("bounce b: waves still running (fraction) / mean active lanes:");
+    for (int b = 0; b < 24; ++b) if (git[b] > 0) printf(" %d:%.3f/%.1f", b, git[b] / gnbw, gact[b] / git[b]);
+    printf("\n");
     printf("cells hist:");
     for (int i = 1; i < 40; ++i) printf(" %d:%.3f", i, tot.hist_cells[i] / q);
     printf("\n");

@@ -1,0 +1,72 @@
+"""Parity on scenes that are not mazes: random soups of axis-aligned rects
+(with the reference's own SAH BVH over them, Scene.bvh).  They exercise what
+the maze does not: thousands of distinct bound values (no dictionary nodes:
+the BVH forms fall back to the top-of-tree cache), grid lists of
+arbitrary rects, and -- in the lattice scene -- many coplanar overlapping
+rects, whose equal hit distances are ties the certified grid search must
+hand to the reference walk.  Bit-exact vs the oracle."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def random_scene(n, seed, lattice):
+    """n axis-aligned rects around the default camera; coordinates on a grid of
+    1/64 (lattice=False) or of 8 (lattice=True: coplanar overlaps everywhere)."""
+    from mirror_maze import Scene
+
+    rng = np.random.default_rng(seed)
+    q = 8.0 if lattice else 1.0 / 64
+    rects = np.zeros((n, 12), np.float32)
+    for i in range(n):
+        k = int(rng.integers(3))
+        iv, iu = [a for a in range(3) if a != k][:: 1 if rng.random() < 0.5 else -1]
+        rects[i, 0:3] = np.round(rng.uniform(-200, 200, 3) / q) * q
+        rects[i, 3 + iv] = max(q, np.round(rng.uniform(2, 40) / q) * q) * rng.choice([-1, 1])
+        rects[i, 6 + iu] = max(q, np.round(rng.uniform(2, 40) / q) * q) * rng.choice([-1, 1])
+        if i % 97 == 0:
+            rects[i, 3:6] = 0.0  # zero-length: never hit (shaders.metal:63)
+        rects[i, 9:12] = rng.uniform(0.2, 0.9, 3)
+    is_mirror = (rng.random(n) < 0.15).astype(np.uint8)
+    emission = np.tile(np.float32([1, 0, 0, 0]), (n, 1))
+    lights = rng.random(n) < 0.1
+    emission[lights] = np.float32([1.0, 0.8, 0.3, 2.0])
+    nodes, idx = Scene.bvh(rects)
+    return Scene(0, rects, nodes, idx, is_mirror, emission, np.zeros((0, 0), np.uint8), 0)
+
+
+@pytest.mark.parametrize("lattice", [False, True], ids=["fine", "lattice"])
+@pytest.mark.parametrize("opts,form,modes", [({}, 11, (11, 12)), ({7: 7}, 7, (6,)), ({7: 5}, 5, (6,)),
+                                             ({7: 5, 9: 0}, 5, (0,))],
+                         ids=["auto-grid", "bvh-lean", "bvh-li", "bvh-li-global"])
+def test_random_scene_windows_bit_exact(gpu, lattice, opts, form, modes):
+    from mirror_maze import (MM_INFO_DICT_OK, MM_INFO_GRID_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE, Renderer,
+                             default_uniform, make_ext)
+    from oracle.oracle import Oracle
+
+    s = random_scene(3000, 11 if lattice else 7, lattice)
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload_scene(s)
+    assert r.scene_info(MM_INFO_GRID_OK) == 1.0
+    assert r.scene_info(MM_INFO_DICT_OK) == (1.0 if lattice else 0.0)
+    u = default_uniform(1920, 1080, 0)
+    e = make_ext(8, 8, 8, frame=3)
+    for (x0, y0) in [(0, 0), (944, 532), (1888, 1064), (300, 800), (1500, 200)]:
+        got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
+        ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
+        assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
+        assert (st.rays, st.paths) == (rst.rays, rst.paths)
+    assert r.scene_info(MM_INFO_LAST_FORM) == form
+    if not lattice:  # the lattice scene's nodes fit the dictionary: mode 10 instead of 6
+        assert r.scene_info(MM_INFO_LAST_LDS_MODE) in modes
+    r.close()
