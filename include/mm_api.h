@@ -170,6 +170,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   <= 256 distinct bound values, 12 B per node) so the whole tree sits in LDS:
                                   1 when the plain nodes do not fit and no explicit split size is set (default),
                                   2 always when it fits (tests), 0 off */
+#define MM_OPT_DEFER      21  /* wave-persistent kernel: once at most this many lanes of a wave still trace
+                                  (past bounce_limit only mirror-hit paths run on), those paths' states are queued
+                                  and a second persistent kernel finishes them 64 to a wave; samples are then
+                                  staged per path and resolved by k_resolve (same order).  0 off, 1..63 */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Facts about the uploaded scene's search structures (double-valued):

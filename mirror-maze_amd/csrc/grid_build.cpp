@@ -5,11 +5,14 @@
 // largest |coordinate|, at least 1), cut into n[a] cells per axis with
 // n[a] = round(extent / s) for a cell size s = the median over the scene's
 // non-degenerate rects of their second-largest extent (the maze's wall
-// height: one cell per maze cell), clamped to 1..256 per axis.
+// height: one cell per maze cell), clamped to 1..256 per axis; s grows by
+// 1.25x until the cells and lists fit the LDS budget the caller gives.
 // Lists: a rect goes on the list of every cell its box comes within eps of;
 // rects that would sit on more than half of the cells (the maze floor) go on
 // the global list every query tests instead (at most 4); zero-length rects
-// (SKIP records: never hit) go nowhere.
+// (SKIP records: never hit) go nowhere.  Rects that are not axis-aligned
+// with exact unit normals (SLOW records) are listed too; the kernel runs the
+// general ray_rect_intersect on them (grid_rect<kSlow>).
 // Per rect the image also holds its compact record (rect_compact.cpp, built
 // with identity slots) and the box of the reference BVH leaf holding it --
 // the box the certificate tests.
@@ -50,38 +53,11 @@ void rect_box(const mm_rect& r, double lo[3], double hi[3]) {
 
 inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 
-}  // namespace
-
-// Returns false (with a reason) when the scene does not suit the search:
-// rects that are not axis-aligned (SLOW records), too many rects or cells.
-bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
-                const uint32_t* idx, GridHost& g, std::string& why) {
-    if (n_rects == 0 || n_rects > 65535) { why = "rect count outside 1..65535"; return false; }
-    std::vector<uint32_t> ident(n_rects), recs;
-    for (uint32_t k = 0; k < n_rects; ++k) ident[k] = k;
-    size_t n_slow = 0;
-    build_compact_rects(rects, n_rects, ident.data(), recs, &n_slow);
-    if (n_slow) { why = "rects that are not axis-aligned"; return false; }
-    // scene box, C, eps, cell size
-    double smin[3] = {INFINITY, INFINITY, INFINITY}, smax[3] = {-INFINITY, -INFINITY, -INFINITY}, C = 1.0;
-    std::vector<double> ext2;
-    for (uint32_t k = 0; k < n_rects; ++k) {
-        double lo[3], hi[3];
-        rect_box(rects[k], lo, hi);
-        double e[3];
-        for (int a = 0; a < 3; ++a) {
-            if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) { why = "non-finite rect"; return false; }
-            smin[a] = std::min(smin[a], lo[a]);
-            smax[a] = std::max(smax[a], hi[a]);
-            C = std::max(C, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
-            e[a] = hi[a] - lo[a];
-        }
-        std::sort(e, e + 3);
-        if (e[1] > 0.0) ext2.push_back(e[1]);
-    }
-    if (ext2.empty()) { why = "no rect with area"; return false; }
-    std::nth_element(ext2.begin(), ext2.begin() + ext2.size() / 2, ext2.end());
-    const double s = ext2[ext2.size() / 2];
+// Cells of size ~s over the scene box widened by eps = C * 2^-14, their lists
+// and the image layout (recs and boxes are filled by the caller).
+bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint32_t>& recs, const double smin[3],
+                 const double smax[3], double C, double s, GridHost& g, std::string& why) {
+    g.n_glob = 0;
     const double eps = C * 0x1p-14;
     long total = 1;
     for (int a = 0; a < 3; ++a) {
@@ -156,6 +132,48 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
                 std::memcpy(&g.image[4 * (size_t)c], &w, 4);
             }
         }
+    }
+    return true;
+}
+
+}  // namespace
+
+// Returns false (with a reason) when the scene does not suit the search (too
+// many rects or cells).  The cell size starts at the scene's typical rect
+// extent and grows by 1.25x until the cells + lists (the part the kernel keeps
+// in LDS) fit index_budget bytes.
+bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
+                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why) {
+    if (n_rects == 0 || n_rects > 65535) { why = "rect count outside 1..65535"; return false; }
+    std::vector<uint32_t> ident(n_rects), recs;
+    for (uint32_t k = 0; k < n_rects; ++k) ident[k] = k;
+    size_t n_slow = 0;
+    build_compact_rects(rects, n_rects, ident.data(), recs, &n_slow);
+    // scene box, C, eps, cell size
+    double smin[3] = {INFINITY, INFINITY, INFINITY}, smax[3] = {-INFINITY, -INFINITY, -INFINITY}, C = 1.0;
+    std::vector<double> ext2;
+    for (uint32_t k = 0; k < n_rects; ++k) {
+        double lo[3], hi[3];
+        rect_box(rects[k], lo, hi);
+        double e[3];
+        for (int a = 0; a < 3; ++a) {
+            if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) { why = "non-finite rect"; return false; }
+            smin[a] = std::min(smin[a], lo[a]);
+            smax[a] = std::max(smax[a], hi[a]);
+            C = std::max(C, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+            e[a] = hi[a] - lo[a];
+        }
+        std::sort(e, e + 3);
+        if (e[1] > 0.0) ext2.push_back(e[1]);
+    }
+    if (ext2.empty()) { why = "no rect with area"; return false; }
+    std::nth_element(ext2.begin(), ext2.begin() + ext2.size() / 2, ext2.end());
+    double s = ext2[ext2.size() / 2];
+    for (int attempt = 0; attempt < 24; ++attempt, s *= 1.25) {
+        if (build_lists(rects, n_rects, recs, smin, smax, C, s, g, why) && 4.0 * g.n[0] * g.n[1] * g.n[2] +
+                                                                                   2.0 * g.n_list <= index_budget)
+            break;
+        if (attempt == 23) { why = "no grid index fits the LDS budget"; return false; }
     }
     std::memcpy(&g.image[g.off_recs], recs.data(), 40u * (size_t)n_rects);
     // the reference leaf box of every rect; a rect in no leaf gets an empty

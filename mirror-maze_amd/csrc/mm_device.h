@@ -18,7 +18,8 @@ constexpr int kStackMax = 50;     // shaders.metal:123
 
 // Closest-hit query methods of the wave-persistent kernel (MM_OPT_TRAVERSAL):
 // BVH loop forms (mm_trace.h) and the certified grid search (mm_grid.h).
-enum : int { kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7, kFormGrid = 11 };
+// kFormGridSlow (internal): the grid search on a scene with SLOW rect records.
+enum : int { kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7, kFormGrid = 11, kFormGridSlow = 12 };
 
 // ---- HBM layouts ------------------------------------------------------------
 // Reference node (nodes_ref): 2 x float4 = the reference's 32-B bvh_node,

@@ -44,12 +44,43 @@ namespace mm {
 // Per-rect compact record test for the search: updates (best, bk, tie) with
 // the rect's a if it is in A (every clause of ray_rect_intersect except
 // a < t).  Records are rect_compact.cpp's FAST records, indexed by rect.
-template <typename R>
-__device__ __forceinline__ void grid_rect(const R& recs, uint32_t k, const Ray& r, float& best, uint32_t& bk,
-                                          bool& tie) {
+// With kSlow, SLOW records (rects without an exact axis-aligned form) run the
+// general statement on the rect geometry (rect_test's operations).
+__device__ __forceinline__ void grid_update(float a, uint32_t k, float& best, uint32_t& bk, bool& tie) {
+    if (a < best) {
+        best = a;
+        bk = k;
+        tie = false;
+    } else if (a == best && k != bk) {
+        tie = true;
+    }
+}
+
+__device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo, uint32_t k, const Ray& r,
+                                                  float& best, uint32_t& bk, bool& tie) {
+    const float4 g0 = geo[4 * k + 0], g1 = geo[4 * k + 1], g2 = geo[4 * k + 2], g3 = geo[4 * k + 3];
+    const F3 o = xyz(g0), n = xyz(g1), v = xyz(g2), u = xyz(g3);
+    const float lv = g0.w, lu = g1.w;
+    const float nc = dot3(r.d, n);
+    const float a = dot3(o - r.o, n) / nc;
+    const F3 rv = (r.o - o) + a * r.d;
+    const float d1 = qdiv(dot3(rv, v), lv, g2.w);
+    const float d2 = qdiv(dot3(rv, u), lu, g3.w);
+    if (d1 >= 0.0f && d1 <= lv && d2 >= 0.0f && d2 <= lu && nc != 0.0f && a > 0.1f) grid_update(a, k, best, bk, tie);
+}
+
+template <bool kSlow, typename R>
+__device__ __forceinline__ void grid_rect(const R& recs, const float4* __restrict__ geo, uint32_t k, const Ray& r,
+                                          float& best, uint32_t& bk, bool& tie) {
     const uint2 w01 = recs[5 * k + 0], w23 = recs[5 * k + 1], w45 = recs[5 * k + 2], w67 = recs[5 * k + 3],
                 w89 = recs[5 * k + 4];
     const uint32_t meta = w89.y;
+    if constexpr (kSlow) {
+        if ((meta >> 30) == 2u) {
+            grid_rect_general(geo, k, r, best, bk, tie);
+            return;
+        }
+    }
     const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
     const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
     const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
@@ -57,15 +88,8 @@ __device__ __forceinline__ void grid_rect(const R& recs, uint32_t k, const Ray& 
     // (a branch-free update measured 6.11 vs 5.86 ms on C3: most tests miss,
     // and the branch skips the update for the whole wave)
     if (x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) && x2 >= __uint_as_float(w67.y) &&
-        x2 <= __uint_as_float(w89.x) && a > 0.1f) {
-        if (a < best) {
-            best = a;
-            bk = k;
-            tie = false;
-        } else if (a == best && k != bk) {
-            tie = true;
-        }
-    }
+        x2 <= __uint_as_float(w89.x) && a > 0.1f)
+        grid_update(a, k, best, bk, tie);
 }
 
 // Where the grid's arrays are read from (LDS or global memory).
@@ -107,13 +131,13 @@ __device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, floa
 // Search + certificate.  Returns true with (t, index) = the reference's answer
 // (t = kBig when nothing is hit), false when the caller must walk the BVH.
 // Requires sc.fast_ok && ray_fast_ok(r) && grid_ray_ok.
-template <bool kStats, typename GV>
-__device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const Ray& r, float& t,
-                                            uint32_t& index, Counters& c) {
+template <bool kStats, bool kSlow, typename GV>
+__device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const float4* __restrict__ geo,
+                                            const Ray& r, float& t, uint32_t& index, Counters& c) {
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
     bool tie = false;
-    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect(gv.recs, g.glob[j], r, best, bk, tie);
+    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect<kSlow>(gv.recs, geo, g.glob[j], r, best, bk, tie);
     int bx = grid_first(g, 0, r.o.x, r.y.x), by = grid_first(g, 1, r.o.y, r.y.y), bz = grid_first(g, 2, r.o.z, r.y.z);
     float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
           tz = grid_time(g, 2, bz, r.o.z, r.y.z);
@@ -128,7 +152,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // is done, step to the next cell (or stop) in the same iteration.
     for (;;) {
         if (j < jend) {
-            grid_rect(gv.recs, (uint32_t)gv.list[j], r, best, bk, tie);
+            grid_rect<kSlow>(gv.recs, geo, (uint32_t)gv.list[j], r, best, bk, tie);
             ++j;
             if (kStats) ++tests;
         }

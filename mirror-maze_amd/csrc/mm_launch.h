@@ -17,6 +17,21 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
                                uint32_t grid_w, uint32_t grid_h, float4* fb, uint32_t* fb8,
                                unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
 
+// Queue of deferred path states, SoA (one array per field, `cap` entries):
+// f[0..11] = ori, dir, T, L (x, y, z each); u[0] seed, u[1] n | mh << 16,
+// u[2] sample slot.  count[0] = slots reserved (the trace kernel's waves
+// reserve with one atomic each; a wave whose reservation would pass `cap`
+// does not defer), count[1] = next entry for the tail kernel, count[2] =
+// tail waves done; the tail kernel's last wave re-zeroes all three.
+struct TailQueue {
+    float* base = nullptr;     // field i at base + i * stride
+    uint32_t stride = 0;
+    uint32_t cap = 0;
+    uint32_t* count = nullptr;
+    __host__ __device__ float* f(int i) const { return base + (size_t)i * stride; }
+    __host__ __device__ uint32_t* u(int i) const { return reinterpret_cast<uint32_t*>(base + (size_t)(12 + i) * stride); }
+};
+
 struct TileJob {
     mm_uniform u;
     mm_ext e;
@@ -38,6 +53,14 @@ struct TileJob {
     uint32_t n_frames = 1;
     // CUs' worth of blocks the wave-persistent grid leaves free (MM_OPT_RESERVE_CUS)
     uint32_t reserve_cus = 0;
+    // Mirror-tail deferral (MM_OPT_DEFER; wave-persistent kernel, samples
+    // staged per path, no fused resolve): a wave whose paths are at bounce
+    // >= defer_from with at most defer_lanes lanes still running queues those
+    // paths' state (ballot + prefix compaction, one atomic per wave) and
+    // moves on; k_trace_tail finishes the queue densely.  Sample slot of a
+    // path: fr * (w*h*spp) + path.  defer_from >= 2^30: off.
+    uint32_t defer_from = 1u << 30, defer_lanes = 0;
+    TailQueue tail;
 };
 
 struct MegaOpts {
@@ -61,6 +84,11 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s);
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
+// The deferred mirror tails of the last wave-persistent launch (same scene data
+// placement and query method): persistent blocks drain job.tail, writing each
+// finished path's sample value to samples[slot].
+hipError_t launch_trace_tail(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
+                             uint32_t* err, bool count_stats, int lds_mode, int form, hipStream_t s);
 
 // ---- wavefront pipeline (trace_wave.hip) ---------------------------------------
 struct WaveState {

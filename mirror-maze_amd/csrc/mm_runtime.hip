@@ -33,7 +33,7 @@ struct GridHost {
     std::vector<uint8_t> image;
 };
 bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
-                const uint32_t* idx, GridHost& g, std::string& why);
+                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why);
 }
 
 struct mm_ctx {
@@ -80,6 +80,9 @@ struct mm_ctx {
     // wavefront SoA state (MM_PIPE_WAVEFRONT)
     void* d_wave = nullptr;
     size_t wave_cap = 0;      // paths
+    // mirror-tail queue (MM_OPT_DEFER)
+    void* d_tail = nullptr;
+    uint32_t tail_cap = 0;
     // aux: stats[4] (u64) + error flag (u32)
     unsigned long long* d_aux = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -96,6 +99,7 @@ struct mm_ctx {
     bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
+    int opt_defer = 0;              // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
@@ -223,6 +227,27 @@ int wave_state(mm_ctx* c, uint32_t n, WaveState& ws) {
     return MM_OK;
 }
 
+// The mirror-tail queue (mm_launch.h TailQueue): 15 SoA arrays of `cap`
+// entries + 3 counters, one allocation; the counters start at zero and the
+// tail kernel's last wave re-zeroes them.
+int tail_queue(mm_ctx* c, uint32_t cap, TailQueue& q) {
+    const size_t n4 = ((size_t)cap + 63) & ~(size_t)63;
+    if (c->tail_cap < cap || !c->d_tail) {
+        (void)hipFree(c->d_tail);
+        c->d_tail = nullptr;
+        c->tail_cap = 0;
+        HIPC(c, hipMalloc(&c->d_tail, (15 * n4 + 64) * 4));
+        HIPC(c, hipMemsetAsync(reinterpret_cast<uint32_t*>(c->d_tail) + 15 * n4, 0, 64 * 4, c->stream));
+        c->tail_cap = cap;
+    }
+    const size_t m4 = ((size_t)c->tail_cap + 63) & ~(size_t)63;
+    q.base = reinterpret_cast<float*>(c->d_tail);
+    q.stride = (uint32_t)m4;
+    q.count = reinterpret_cast<uint32_t*>(c->d_tail) + 15 * m4;
+    q.cap = c->tail_cap;
+    return MM_OK;
+}
+
 int begin_timing(mm_ctx* c) {
     HIPC(c, hipEventRecord(c->ev0, c->stream));
     return MM_OK;
@@ -300,7 +325,7 @@ void mm_destroy(mm_ctx* c) {
     free_scene(c);
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
-    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave);
+    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave); (void)hipFree(c->d_tail);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -362,6 +387,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_RESERVE_CUS:
             if (value < 0 || value > 128) return fail(c, MM_ERR_INVALID, "reserved CUs must be 0..128");
             c->opt_reserve_cus = (uint32_t)value;
+            return MM_OK;
+        case MM_OPT_DEFER:
+            if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "defer lanes must be 0..63");
+            c->opt_defer = value;
             return MM_OK;
         case MM_OPT_DICT_NODES:
             if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
@@ -502,9 +531,9 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     // certified grid search (mm_grid.h): needs the Markstein guards and axis-aligned rects
     GridHost gh;
     std::string gwhy;
-    const bool grid_ok = fast && n_slow == 0 && build_grid(rects, n_rects, nodes, n_nodes, idx, gh, gwhy);
+    // (80 KB: the LDS of one of the two 1024-thread blocks per CU)
+    const bool grid_ok = fast && build_grid(rects, n_rects, nodes, n_nodes, idx, 80 * 1024, gh, gwhy);
     if (!fast) gwhy = "scene coordinates outside the exact-division guards";
-    if (fast && n_slow) gwhy = "rects that are not axis-aligned";
     DevGrid dg{};
     if (grid_ok) {
         HIPC(c, hipMalloc((void**)&c->d_grid, gh.bytes));
@@ -660,6 +689,7 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
     if (form == kFormGrid) {
         if (!c->grid_ok)
             return fail(c, MM_ERR_UNSUPPORTED, "grid search unavailable for this scene: " + c->grid_why);
+        if (!c->lean_ok) form = kFormGridSlow;  // general rect tests for the SLOW records
         if (c->opt_lds && c->grid.bytes <= budget) { mode = 11; return MM_OK; }
         if (c->opt_lds && c->grid.off_recs <= budget) { mode = 12; return MM_OK; }
         if (!auto_form || !c->opt_lds) { mode = 13; return MM_OK; }
@@ -720,17 +750,21 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     // staging buffer: one launch covers up to 2^31 paths (a whole C5 frame).
     const uint64_t row_paths = (uint64_t)w * e->spp;
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
+    const bool persist = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2;
+    // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run by k_trace_tail
+    const bool defer = persist && c->opt_defer > 0;
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
-    const bool fuse = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2 && c->opt_fuse && 64 % e->spp == 0;
-    const uint64_t batch_paths = fuse ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
+    const bool fuse = persist && !defer && c->opt_fuse && 64 % e->spp == 0;
+    const uint64_t batch_paths = (fuse || defer) ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
     if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
     if (n_frames > 1) {
-        // several frames in one launch: the wave-persistent kernel's queue with the fused resolve
-        if (!fuse)
+        // several frames in one launch: the wave-persistent kernel's queue, with the fused resolve or
+        // (tail deferral) samples staged per frame
+        if (!fuse && !defer)
             return fail(c, MM_ERR_UNSUPPORTED, "mm_trace_tile_frames: needs the wave-persistent kernel with the "
-                                               "fused resolve (64 % spp == 0)");
+                                               "fused resolve (64 % spp == 0) or tail deferral");
         if (e->flags & MM_EXT_ACCUMULATE)
             return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: frames of one launch cannot accumulate into "
                                            "one image");
@@ -738,8 +772,15 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         if (rows_per_batch < h || queue + (1ull << 24) > 0xFFFFFFFFull)
             return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: more paths than one launch holds (2^32)");
     }
-    int rc = fuse ? MM_OK : ensure(c, c->d_samples, c->samples_cap, (size_t)(row_paths * rows_per_batch));
+    int rc = fuse ? MM_OK : ensure(c, c->d_samples, c->samples_cap,
+                                   (size_t)(row_paths * rows_per_batch) * (defer ? n_frames : 1));
     if (rc) return rc;
+    TailQueue tq;
+    if (defer) {  // queue capacity: a quarter of the paths (a wave past it does not defer)
+        const uint32_t cap = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull >> 2,
+                                                          row_paths * rows_per_batch * n_frames / 4 + 65536);
+        if ((rc = tail_queue(c, cap, tq))) return rc;
+    }
     // aux: [0..3] stats (zeroed only when counted), [4] sticky error flag
     // (cleared by read_aux), [5] lane-refill counter (zeroed by its launcher),
     // [6] wave-persistent counter pair (self-cleaning).  No fill kernel on the
@@ -763,6 +804,11 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
         job.reserve_cus = c->opt_reserve_cus;
+        if (defer) {
+            job.defer_from = 1;
+            job.defer_lanes = (uint32_t)c->opt_defer;
+            job.tail = tq;
+        }
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
         if (wave) {
@@ -788,12 +834,17 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             int form = 0, mode = 0;
             DevScene sc = dev_scene(c);
             if ((rc = choose_wavepersist(c, sc, form, mode))) return rc;
-            c->last_form = form;
+            c->last_form = form == kFormGridSlow ? kFormGrid : form;
             c->last_mode = mode;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
                                              c->stream));
+            if (defer) {
+                HIPC(c, launch_trace_tail(sc, job, c->d_samples, c->d_aux, reinterpret_cast<uint32_t*>(c->d_aux + 4),
+                                          want_stats, mode, form, c->stream));
+                launches += 1;
+            }
         } else {
             MegaOpts mo;
             mo.reference = c->pipe == MM_PIPE_REFERENCE;
@@ -807,8 +858,13 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             launches += 1;
             continue;
         }
-        HIPC(c, launch_resolve(job, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
-        launches += 2;
+        const size_t fpaths = (size_t)job.w * job.h * job.e.spp, fpix = (size_t)job.w * job.h;
+        for (uint32_t f = 0; f < (defer ? n_frames : 1u); ++f) {  // frame f's samples -> its output slice
+            HIPC(c, launch_resolve(job, c->d_samples + f * fpaths,
+                                   reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w + f * fpix, c->stream));
+            launches += 1;
+        }
+        launches += 1;
     }
     if ((rc = end_timing(c, launches))) return rc;
     if (want_stats) return read_aux(c, stats);

@@ -150,6 +150,31 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // 64 % spp == 0 the wave's 64 paths are whole pixels and it resolves them
 // itself (job.fuse).  A multi-frame launch queues frame 0's chunks, then frame
 // 1's, ...; a chunk's frame picks its RNG frame and output slice.
+//
+// Mirror-tail deferral (job.defer_from < 2^30): once at most defer_lanes of a
+// wave's 64 lanes still run -- past bounce_limit only paths that hit mirrors
+// continue (shaders.metal:306, `n < bounce_limit + mirror_hits`) -- those
+// lanes queue their path state and the wave takes a new chunk; k_trace_tail
+// then runs the queued tails 64 to a wave.  On C3 a
+// wave otherwise spends ~27 % of its bounce iterations on <= 12 live lanes
+// (scripts/grid_sim.c).  Samples are then staged per path and resolved by
+// k_resolve (the same operations in the same order as the fused resolve).
+
+// A deferred path's state into its reserved queue entry.
+__device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t i, const PathState& p, uint32_t slot) {
+    q.f(0)[i] = p.ori.x; q.f(1)[i] = p.ori.y; q.f(2)[i] = p.ori.z;
+    q.f(3)[i] = p.dir.x; q.f(4)[i] = p.dir.y; q.f(5)[i] = p.dir.z;
+    q.f(6)[i] = p.T.x; q.f(7)[i] = p.T.y; q.f(8)[i] = p.T.z;
+    q.f(9)[i] = p.L.x; q.f(10)[i] = p.L.y; q.f(11)[i] = p.L.z;
+    q.u(0)[i] = p.seed;
+    q.u(1)[i] = (uint32_t)p.n | ((uint32_t)p.mh << 16);
+    q.u(2)[i] = slot;
+}
+
+__device__ __forceinline__ F3 path_value(const PathState& p) {
+    return F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))};
+}
+
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
                                                      float4* __restrict__ samples, unsigned long long* stats,
@@ -178,14 +203,27 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             const uint32_t pix = path / spp, smp = path - pix * spp;
             const uint32_t j = pix / job.w, i = pix - j * job.w;
             const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
-            uint32_t seed = seed_tile(py * job.view_w + px, smp, job.e.frame + fr);
-            const F3 d = jitter(primary_dir(job.u, px, py), seed);
+            PathState p;
+            p.seed = seed_tile(py * job.view_w + px, smp, job.e.frame + fr);
+            p.dir = jitter(primary_dir(job.u, px, py), p.seed);
+            p.ori = ori;
+            p.T = F3{1.0f, 1.0f, 1.0f};
+            p.L = F3{0.0f, 0.0f, 0.0f};
+            p.n = 0;
+            p.mh = 0;
             bool overflow = false;
-            s = trace_path<kStats>(sc, q, ori, d, seed, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c,
-                                   overflow);
+            uint32_t qi = 0;
+            const bool deferred = bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit,
+                                                      stack, c, overflow, (int)job.defer_from, job.defer_lanes,
+                                                      job.tail.count, job.tail.cap, &qi);
             if (overflow) atomicOr(err, 1u);
-            if (!job.fuse) samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
-            paths++;
+            const uint32_t slot = fr * n_paths + path;
+            if (deferred) tail_store(job.tail, qi, p, slot);
+            if (!deferred) {
+                s = path_value(p);
+                if (!job.fuse) samples[slot] = make_float4(s.x, s.y, s.z, 0.0f);
+                paths++;
+            }
         }
         if (job.fuse) resolve_in_wave(job, s, path, valid, job.out + (size_t)fr * job.w * job.h);
     }
@@ -193,9 +231,50 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     return chunks;
 }
 
+// The deferred tails: waves take 64 queued paths at a time and finish them.
+template <bool kStats, typename Q>
+__device__ __forceinline__ uint32_t tail_body(const DevScene& sc, const Q& q, const TileJob& job,
+                                              float4* __restrict__ samples, unsigned long long* stats,
+                                              uint32_t* err, uint32_t*) {
+    const TailQueue& tq = job.tail;
+    const uint32_t n = min(tq.count[0], tq.cap);  // reservations past cap were not used
+    const uint32_t lane = threadIdx.x & 63u;
+    Counters c;
+    ScratchStack stack;
+    uint32_t paths = 0, chunks = 0;
+    for (;;) {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(tq.count + 1, 64u);
+        const uint32_t base = __builtin_amdgcn_readfirstlane(b);
+        if (base >= n) break;
+        ++chunks;
+        const uint32_t i = base + lane;
+        if (i < n) {
+            PathState p;
+            p.ori = F3{tq.f(0)[i], tq.f(1)[i], tq.f(2)[i]};
+            p.dir = F3{tq.f(3)[i], tq.f(4)[i], tq.f(5)[i]};
+            p.T = F3{tq.f(6)[i], tq.f(7)[i], tq.f(8)[i]};
+            p.L = F3{tq.f(9)[i], tq.f(10)[i], tq.f(11)[i]};
+            p.seed = tq.u(0)[i];
+            const uint32_t nm = tq.u(1)[i];
+            p.n = (int)(nm & 0xFFFFu);
+            p.mh = (int)(nm >> 16);
+            bool overflow = false;
+            bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
+                                1 << 30, 0u);
+            if (overflow) atomicOr(err, 1u);
+            const F3 s = path_value(p);
+            samples[tq.u(2)[i]] = make_float4(s.x, s.y, s.z, 0.0f);
+            paths++;
+        }
+    }
+    if (kStats) flush_stats(stats, c, paths);
+    return chunks;
+}
+
 // LDS modes (what a resident block stages before tracing; the rest is read
 // through L1/L2):
-//   0  nothing (nodes, records global)           BVH forms 0 / 5
+//   0  nothing (nodes, records global)           BVH forms 5
 //   1  BVH nodes                                  BVH forms 0 / 5 (general rect test)
 //   3  BVH nodes + compact slot records           BVH forms 0 / 5 / 7
 //   6  top of the breadth-first node array        BVH forms 5 / 7 (split cache)
@@ -204,89 +283,82 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
 //   11 the whole grid image                       grid search
 //   12 grid cells + lists, records + boxes global grid search
 //   13 nothing (the grid image global)             grid search
-#define MM_TS_STAGED()                                                                                      \
-    do {                                                                                                     \
-        if (job.wave_ts && (threadIdx.x & 63u) == 0) {                                                       \
-            const uint32_t wid_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                      \
-            if (wid_ < job.wave_ts_cap) job.wave_ts[4 * wid_ + 1] = (unsigned long long)wall_clock64();     \
-        }                                                                                                    \
-    } while (0)
-
-template <bool kStats, int kLds, int kForm>
-// 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
-// 768-thread blocks at 6 waves (80 VGPRs, no VGPR spills) measured 6.21 vs
-// 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).
-__global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
-                                                               unsigned long long* stats, uint32_t* err,
-                                                               uint32_t* work) {
-    const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
-    uint32_t chunks = 0;
+// stage_and_run fills the block's LDS for the mode and calls body(query).
+template <int kLds, int kForm, bool kStats, typename F>
+__device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const TileJob& job, F&& body) {
     extern __shared__ float4 lds[];
+    auto staged = [&]() {  // diagnostics: time at which the block's LDS staging completed (wave timeline)
+        if (job.wave_ts && (threadIdx.x & 63u) == 0) {
+            const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            if (wid < job.wave_ts_cap) job.wave_ts[4 * wid + 1] = (unsigned long long)wall_clock64();
+        }
+    };
     if constexpr (kLds == 11 || kLds == 12) {
         const uint32_t n16 = (kLds == 11 ? sc.grid.bytes : sc.grid.off_recs) / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
         for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) img[i] = sc.grid.image[i];
         __syncthreads();
-        MM_TS_STAGED();
+        staged();
         const char* base = reinterpret_cast<const char*>(lds);
         const uint32_t* cells = reinterpret_cast<const uint32_t*>(base);
         const uint16_t* list = reinterpret_cast<const uint16_t*>(base + sc.grid.off_list);
         if constexpr (kLds == 11) {
             const auto gv = grid_view(cells, list, reinterpret_cast<const uint2*>(base + sc.grid.off_recs),
                                       reinterpret_cast<const float2*>(base + sc.grid.off_box));
-            chunks = wavepersist_body<kStats>(sc, GridQuery<kStats, decltype(gv)>{sc, gv}, job, samples, stats, err,
-                                              work);
+            return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
         } else {
             const auto gv = grid_view(cells, list, sc.grid.recs, sc.grid.box);
-            chunks = wavepersist_body<kStats>(sc, GridQuery<kStats, decltype(gv)>{sc, gv}, job, samples, stats, err,
-                                              work);
+            return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
         }
     } else if constexpr (kLds == 13) {
         const auto gv = grid_view(sc.grid.cells, sc.grid.list, sc.grid.recs, sc.grid.box);
-        chunks = wavepersist_body<kStats>(sc, GridQuery<kStats, decltype(gv)>{sc, gv}, job, samples, stats, err,
-                                          work);
+        return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 6) {
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
         __syncthreads();
-        MM_TS_STAGED();
+        staged();
         const auto v = view(SplitNodes{lds, sc.nodes, sc.n_lds_f4}, sc.recs);
-        chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats, err,
-                                          work);
+        return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
     } else if constexpr (kLds == 10) {
         float* tab = reinterpret_cast<float*>(lds);
         uint32_t* words = reinterpret_cast<uint32_t*>(tab + 256);
         for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = sc.dict_tab[i];
         for (uint32_t i = threadIdx.x; i < 3 * sc.n_nodes; i += blockDim.x) words[i] = sc.dict_words[i];
         __syncthreads();
-        MM_TS_STAGED();
+        staged();
         const auto v = view(DictNodes{words, tab}, sc.recs);
-        chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats, err,
-                                          work);
+        return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
     } else if constexpr (kLds == 1 || kLds == 3 || kLds == 7) {
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds[i] = sc.nodes[i];
         uint2* lds_recs = reinterpret_cast<uint2*>(lds + 2 * sc.n_nodes);
         if constexpr (kLds == 3)
             for (uint32_t i = threadIdx.x; i < 5 * sc.n_rects; i += blockDim.x) lds_recs[i] = sc.recs[i];
         __syncthreads();
-        MM_TS_STAGED();
+        staged();
         if constexpr (kLds == 3) {
             const auto v = view(static_cast<float4*>(lds), lds_recs);
-            chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats,
-                                              err, work);
+            return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
         } else if constexpr (kLds == 7) {
             const auto v = view(static_cast<float4*>(lds), sc.recs);
-            chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats,
-                                              err, work);
+            return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
         } else {
             const auto v = view(static_cast<float4*>(lds));
-            chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats,
-                                              err, work);
+            return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
         }
     } else {
         const auto v = view(sc.nodes);
-        chunks = wavepersist_body<kStats>(sc, BvhQuery<kStats, kForm, decltype(v)>{sc, v}, job, samples, stats, err,
-                                          work);
+        return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
     }
+}
+
+// Per-wave diagnostics record and the self-cleaning counter pair shared by the
+// persistent kernels (counter[0] = next item, counter[1] = waves done; the
+// last wave to finish re-zeroes the words, so the next launch needs no memset
+// -- a fill kernel queued between two frames on another stream would wait for
+// free CUs and serialise overlapping frames).  `extra` (or null): a third word
+// the last wave also clears (the tail queue's entry count).
+__device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chunks, unsigned long long t_entry,
+                                                uint32_t* counter, uint32_t* extra) {
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (wid < job.wave_ts_cap) {
@@ -295,18 +367,38 @@ __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, Tile
             job.wave_ts[4 * wid + 3] = chunks;
         }
     }
-    // Self-cleaning work counter (work[0] = next path, work[1] = waves done):
-    // the last wave to finish re-zeroes both, so the next launch needs no
-    // memset -- a fill kernel queued between two frames on another stream
-    // would wait for free CUs and serialise overlapping frames.
     if ((threadIdx.x & 63u) == 0) {
         __threadfence();
         const uint32_t total = gridDim.x * (blockDim.x >> 6);
-        if (atomicAdd(work + 1, 1u) == total - 1) {
-            atomicExch(work, 0u);
-            atomicExch(work + 1, 0u);
+        if (atomicAdd(counter + 1, 1u) == total - 1) {
+            atomicExch(counter, 0u);
+            atomicExch(counter + 1, 0u);
+            if (extra) atomicExch(extra, 0u);
         }
     }
+}
+
+// 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
+// 768-thread blocks at 6 waves (80 VGPRs, no VGPR spills) measured 6.21 vs
+// 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).
+template <bool kStats, int kLds, int kForm>
+__global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                               unsigned long long* stats, uint32_t* err,
+                                                               uint32_t* work) {
+    const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
+    const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
+        return wavepersist_body<kStats>(sc, q, job, samples, stats, err, work);
+    });
+    persistent_exit(job, chunks, t_entry, work, nullptr);
+}
+
+template <bool kStats, int kLds, int kForm>
+__global__ __launch_bounds__(1024, 8) void k_trace_tail(DevScene sc, TileJob job, float4* __restrict__ samples,
+                                                        unsigned long long* stats, uint32_t* err) {
+    const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
+        return tail_body<kStats>(sc, q, job, samples, stats, err, nullptr);
+    });
+    persistent_exit(job, chunks, 0ull, job.tail.count + 1, job.tail.count);
 }
 
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
@@ -321,37 +413,67 @@ size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
     }
 }
 
+// Resident grid of a persistent kernel: blocks per CU from the occupancy API x
+// CUs (minus MM_OPT_RESERVE_CUS), capped by the work.
+template <typename K>
+static uint32_t persistent_grid(K kern, size_t lds, uint32_t reserve_cus, uint64_t items) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 1024, lds) != hipSuccess) return 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus_used = std::max(1, cus - (int)reserve_cus);
+    uint64_t grid = (uint64_t)std::max(1, per_cu) * (uint64_t)cus_used;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, (items + 1023) / 1024));
+}
+
 template <int kLds, int kForm>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        hipStream_t s) {
-    constexpr uint32_t block = 1024;
     const size_t lds = wavepersist_lds_bytes(sc, kLds);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm> : k_trace_wavepersist<false, kLds, kForm>;
-    int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, (int)block, lds);
-    if (e != hipSuccess) return e;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t n_paths = (uint64_t)job.w * job.h * job.e.spp * job.n_frames;
-    // MM_OPT_RESERVE_CUS: leave that many CUs' worth of resident blocks free for other work (collectives)
-    const int cus_used = std::max(1, cus - (int)job.reserve_cus);
-    uint64_t grid = (uint64_t)std::max(1, per_cu) * (uint64_t)cus_used;
-    grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, (n_paths + block - 1) / block));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(block), lds, s, sc, job, samples, stats, err, work);
+    const uint32_t grid =
+        persistent_grid(kern, lds, job.reserve_cus, (uint64_t)job.w * job.h * job.e.spp * job.n_frames);
+    if (!grid) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, s, sc, job, samples, stats, err, work);
     return hipGetLastError();
 }
+
+template <int kLds, int kForm>
+static hipError_t launch_tail_t(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
+                                uint32_t* err, bool count_stats, hipStream_t s) {
+    const size_t lds = wavepersist_lds_bytes(sc, kLds);
+    auto kern = count_stats ? k_trace_tail<true, kLds, kForm> : k_trace_tail<false, kLds, kForm>;
+    // the queue length is known on the device only: a full resident grid (each wave drains 64 at a time)
+    const uint32_t grid = persistent_grid(kern, lds, job.reserve_cus, ~0ull >> 1);
+    if (!grid) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, s, sc, job, samples, stats, err);
+    return hipGetLastError();
+}
+
+#define MM_WP_INSTANCES(X)                                                                                    \
+    X(11, kFormGrid) X(12, kFormGrid) X(13, kFormGrid)                                                        \
+    X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
+    X(3, kFormLean) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                          \
+    X(0, kFormLeafInterior) X(1, kFormLeafInterior) X(3, kFormLeafInterior) X(6, kFormLeafInterior)           \
+    X(7, kFormLeafInterior) X(10, kFormLeafInterior)                                                          \
+    X(1, kFormIfIf) X(3, kFormIfIf)
 
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s) {
 #define MM_WP(L, F) \
     if (lds_mode == L && form == F) return launch_wavepersist_t<L, F>(sc, job, samples, stats, err, work, count_stats, s);
-    MM_WP(11, kFormGrid) MM_WP(12, kFormGrid) MM_WP(13, kFormGrid)
-    MM_WP(3, kFormLean) MM_WP(6, kFormLean) MM_WP(7, kFormLean) MM_WP(10, kFormLean)
-    MM_WP(0, kFormLeafInterior) MM_WP(1, kFormLeafInterior) MM_WP(3, kFormLeafInterior) MM_WP(6, kFormLeafInterior)
-    MM_WP(7, kFormLeafInterior) MM_WP(10, kFormLeafInterior)
-    MM_WP(1, kFormIfIf) MM_WP(3, kFormIfIf)
+    MM_WP_INSTANCES(MM_WP)
+#undef MM_WP
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_trace_tail(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
+                             uint32_t* err, bool count_stats, int lds_mode, int form, hipStream_t s) {
+#define MM_WP(L, F) \
+    if (lds_mode == L && form == F) return launch_tail_t<L, F>(sc, job, samples, stats, err, count_stats, s);
+    MM_WP_INSTANCES(MM_WP)
 #undef MM_WP
     return hipErrorInvalidValue;
 }

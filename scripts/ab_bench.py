@@ -31,6 +31,10 @@ VARIANTS = {
     "bvh-li-split": (1, {7: 5, 9: 80}),
     "mega-lds": (1, {3: 0, 1: 1}),
     "nofuse": (1, {12: 0}),
+    "defer8": (1, {21: 8}),
+    "defer16": (1, {21: 16}),
+    "defer32": (1, {21: 32}),
+    "defer48": (1, {21: 48}),
     "wave": (2, {}),
     "ref": (3, {}),
 }
@@ -63,7 +67,7 @@ def main():
             for k, v in opts.items():
                 r.set_option(k, v)
             r.upload_scene(scene)
-            multi = pipe in (0, 1) and opts.get(12, 1) and opts.get(3, 2) == 2 and 64 % spp == 0
+            multi = pipe in (0, 1) and opts.get(3, 2) == 2 and (opts.get(21, 0) or (opts.get(12, 1) and 64 % spp == 0))
             out = torch.zeros((a.frames, h, W, 4), dtype=torch.float32, device="cuda")
             _, st = r.trace_tile(u, make_ext(spp, bl, ml, frame=0), 0, 0, W, h, y_stride=a.ranks, out=out[0],
                                  stats=True)  # warm; rays of frame 0

@@ -29,16 +29,20 @@ def _diff(got, ref):
     return int(bad.sum())
 
 
-def test_c3_bench_path_two_whole_frames(gpu):
+@pytest.mark.parametrize("opts", [{}, {21: 16}], ids=["default", "tail-defer16"])
+def test_c3_bench_path_two_whole_frames(gpu, opts):
     """C3 exactly as bench.py renders it: MM_PIPE_AUTO (the grid search), two
     consecutive frames in ONE mm_trace_tile_frames launch, every pixel of
-    both 1920x1080 frames (2 x 137 M closest-hit queries) vs the oracle."""
+    both 1920x1080 frames (2 x 137 M closest-hit queries) vs the oracle --
+    with the library defaults and with mirror-tail deferral."""
     from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 
     s = _scene(32)
     r = Renderer(0)
     r.set_pipeline(MM_PIPE_AUTO)
+    for k, v in opts.items():
+        r.set_option(k, v)
     r.upload_scene(s)
     u = default_uniform(1920, 1080, 0)
     e = make_ext(8, 8, 8, frame=0)

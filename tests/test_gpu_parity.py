@@ -115,6 +115,9 @@ PIPES = {
     "auto": (0, {}, False),                                  # grid search (C3 default)
     "grid": (1, {7: 11}, False),
     "grid-nofuse": (1, {7: 11, 12: 0}, False),
+    "grid-defer16": (1, {21: 16}, False),
+    "grid-defer63": (1, {21: 63}, False),
+    "bvh-lean-defer32": (1, {7: 7, 21: 32}, True),
     "bvh-lean-ldsrects": (1, {7: 7}, True),
     "bvh-lean-globalrecs": (1, {7: 7, 8: 0}, True),
     "bvh-lean-split2kb": (1, {7: 7, 9: 2}, True),
@@ -170,8 +173,8 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
     ren.close()
 
 
-@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "bvh-lean-ldsrects", "bvh-li-dict", "mega-lds",
-                                  "wavefront"])
+@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-defer16", "bvh-lean-ldsrects", "bvh-li-dict",
+                                  "mega-lds", "wavefront"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -215,7 +218,7 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}])
+@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 16}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole

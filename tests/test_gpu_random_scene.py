@@ -42,15 +42,27 @@ def random_scene(n, seed, lattice):
     return Scene(0, rects, nodes, idx, is_mirror, emission, np.zeros((0, 0), np.uint8), 0)
 
 
+# per scene: options -> (query method run, LDS modes it may use) or None when the
+# method is unavailable (form 7 needs a compact record for every rect: the fine
+# scene's rects have normals that are not exactly +-1, SLOW records)
+CASES = {
+    "auto-grid": ({}, {False: (11, (11, 12)), True: (11, (11, 12))}),
+    "bvh-lean": ({7: 7}, {False: None, True: (7, (10,))}),
+    "bvh-li": ({7: 5}, {False: (5, (6,)), True: (5, (10,))}),
+    "bvh-li-nodict": ({7: 5, 20: 0, 9: 0}, {False: (5, (0,)), True: (5, (0,))}),
+    "grid-global": ({7: 11, 1: 0}, {False: (11, (13,)), True: (11, (13,))}),
+}
+
+
 @pytest.mark.parametrize("lattice", [False, True], ids=["fine", "lattice"])
-@pytest.mark.parametrize("opts,form,modes", [({}, 11, (11, 12)), ({7: 7}, 7, (6,)), ({7: 5}, 5, (6,)),
-                                             ({7: 5, 9: 0}, 5, (0,))],
-                         ids=["auto-grid", "bvh-lean", "bvh-li", "bvh-li-global"])
-def test_random_scene_windows_bit_exact(gpu, lattice, opts, form, modes):
-    from mirror_maze import (MM_INFO_DICT_OK, MM_INFO_GRID_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE, Renderer,
-                             default_uniform, make_ext)
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_random_scene_windows_bit_exact(gpu, lattice, case):
+    from mirror_maze import (MM_INFO_DICT_OK, MM_INFO_GRID_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE,
+                             MM_INFO_LEAN, MMError, Renderer, default_uniform, make_ext)
     from oracle.oracle import Oracle
 
+    opts, expect = CASES[case]
+    expect = expect[lattice]
     s = random_scene(3000, 11 if lattice else 7, lattice)
     o = Oracle.from_scene(s)
     r = Renderer(0)
@@ -59,14 +71,19 @@ def test_random_scene_windows_bit_exact(gpu, lattice, opts, form, modes):
     r.upload_scene(s)
     assert r.scene_info(MM_INFO_GRID_OK) == 1.0
     assert r.scene_info(MM_INFO_DICT_OK) == (1.0 if lattice else 0.0)
+    assert r.scene_info(MM_INFO_LEAN) == (1.0 if lattice else 0.0)
     u = default_uniform(1920, 1080, 0)
     e = make_ext(8, 8, 8, frame=3)
+    if expect is None:
+        with pytest.raises(MMError):
+            r.trace_tile(u, e, 0, 0, 32, 16)
+        r.close()
+        return
     for (x0, y0) in [(0, 0), (944, 532), (1888, 1064), (300, 800), (1500, 200)]:
         got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
         ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
         assert (st.rays, st.paths) == (rst.rays, rst.paths)
-    assert r.scene_info(MM_INFO_LAST_FORM) == form
-    if not lattice:  # the lattice scene's nodes fit the dictionary: mode 10 instead of 6
-        assert r.scene_info(MM_INFO_LAST_LDS_MODE) in modes
+    assert r.scene_info(MM_INFO_LAST_FORM) == expect[0]
+    assert r.scene_info(MM_INFO_LAST_LDS_MODE) in expect[1]
     r.close()
