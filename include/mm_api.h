@@ -173,7 +173,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_DEFER      21  /* wave-persistent kernel: once at most this many lanes of a wave still trace
                                   (past bounce_limit only mirror-hit paths run on), those paths' states are queued
                                   and a second persistent kernel finishes them 64 to a wave; samples are then
-                                  staged per path and resolved by k_resolve (same order).  0 off, 1..63 */
+                                  staged per path and resolved by k_resolve (same order).  0 off, 1..63;
+                                  default 16 (C3 5.92 -> 5.64 ms, profiles/r02_ab_defer.txt).  Built for the grid
+                                  search and the lean BVH form with records in LDS; other forms ignore it */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Facts about the uploaded scene's search structures (double-valued):

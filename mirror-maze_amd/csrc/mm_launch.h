@@ -84,6 +84,8 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s);
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
+// Whether the tail-deferral variant exists for this (LDS mode, form).
+bool wavepersist_defer_built(int lds_mode, int form);
 // The deferred mirror tails of the last wave-persistent launch (same scene data
 // placement and query method): persistent blocks drain job.tail, writing each
 // finished path's sample value to samples[slot].

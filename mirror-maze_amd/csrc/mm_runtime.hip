@@ -99,7 +99,7 @@ struct mm_ctx {
     bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
-    int opt_defer = 0;              // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
+    int opt_defer = 16;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
@@ -751,8 +751,15 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     const uint64_t row_paths = (uint64_t)w * e->spp;
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
     const bool persist = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2;
-    // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run by k_trace_tail
-    const bool defer = persist && c->opt_defer > 0;
+    int form = 0, mode = 0;
+    DevScene sc = dev_scene(c);
+    if (persist) {
+        int rc0 = choose_wavepersist(c, sc, form, mode);
+        if (rc0) return rc0;
+    }
+    // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run by k_trace_tail; built for
+    // the grid search and the lean BVH form with records in LDS (other forms run without it)
+    const bool defer = persist && c->opt_defer > 0 && wavepersist_defer_built(mode, form);
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
     const bool fuse = persist && !defer && c->opt_fuse && 64 % e->spp == 0;
     const uint64_t batch_paths = (fuse || defer) ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
@@ -830,10 +837,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                 launches += 2;
             }
             launches += 1;
-        } else if (c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2) {
-            int form = 0, mode = 0;
-            DevScene sc = dev_scene(c);
-            if ((rc = choose_wavepersist(c, sc, form, mode))) return rc;
+        } else if (persist) {
             c->last_form = form == kFormGridSlow ? kFormGrid : form;
             c->last_mode = mode;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,

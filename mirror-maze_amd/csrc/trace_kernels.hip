@@ -175,7 +175,7 @@ __device__ __forceinline__ F3 path_value(const PathState& p) {
     return F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))};
 }
 
-template <bool kStats, typename Q>
+template <bool kStats, bool kDefer, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
                                                      float4* __restrict__ samples, unsigned long long* stats,
                                                      uint32_t* err, uint32_t* work) {
@@ -213,9 +213,14 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             p.mh = 0;
             bool overflow = false;
             uint32_t qi = 0;
-            const bool deferred = bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit,
-                                                      stack, c, overflow, (int)job.defer_from, job.defer_lanes,
-                                                      job.tail.count, job.tail.cap, &qi);
+            bool deferred = false;
+            if constexpr (kDefer)
+                deferred = bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c,
+                                               overflow, (int)job.defer_from, job.defer_lanes, job.tail.count,
+                                               job.tail.cap, &qi);
+            else
+                bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
+                                    1 << 30, 0u);
             if (overflow) atomicOr(err, 1u);
             const uint32_t slot = fr * n_paths + path;
             if (deferred) tail_store(job.tail, qi, p, slot);
@@ -381,13 +386,13 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
 // 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
 // 768-thread blocks at 6 waves (80 VGPRs, no VGPR spills) measured 6.21 vs
 // 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).
-template <bool kStats, int kLds, int kForm>
+template <bool kStats, int kLds, int kForm, bool kDefer>
 __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
     const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
-        return wavepersist_body<kStats>(sc, q, job, samples, stats, err, work);
+        return wavepersist_body<kStats, kDefer>(sc, q, job, samples, stats, err, work);
     });
     persistent_exit(job, chunks, t_entry, work, nullptr);
 }
@@ -426,12 +431,13 @@ static uint32_t persistent_grid(K kern, size_t lds, uint32_t reserve_cus, uint64
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, (items + 1023) / 1024));
 }
 
-template <int kLds, int kForm>
+template <int kLds, int kForm, bool kDefer>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        hipStream_t s) {
     const size_t lds = wavepersist_lds_bytes(sc, kLds);
-    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm> : k_trace_wavepersist<false, kLds, kForm>;
+    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm, kDefer>
+                            : k_trace_wavepersist<false, kLds, kForm, kDefer>;
     const uint32_t grid =
         persistent_grid(kern, lds, job.reserve_cus, (uint64_t)job.w * job.h * job.e.spp * job.n_frames);
     if (!grid) return hipErrorInvalidValue;
@@ -451,19 +457,37 @@ static hipError_t launch_tail_t(const DevScene& sc, const TileJob& job, float4* 
     return hipGetLastError();
 }
 
-#define MM_WP_INSTANCES(X)                                                                                    \
+// (LDS mode, form) pairs; the tail-deferral variant (MM_OPT_DEFER) is built
+// for the grid search and the lean BVH form with records in LDS
+#define MM_DEFER_INSTANCES(X)                                                                                 \
     X(11, kFormGrid) X(12, kFormGrid) X(13, kFormGrid)                                                        \
     X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
-    X(3, kFormLean) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                          \
+    X(3, kFormLean)
+#define MM_WP_INSTANCES(X)                                                                                    \
+    MM_DEFER_INSTANCES(X) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                    \
     X(0, kFormLeafInterior) X(1, kFormLeafInterior) X(3, kFormLeafInterior) X(6, kFormLeafInterior)           \
     X(7, kFormLeafInterior) X(10, kFormLeafInterior)                                                          \
     X(1, kFormIfIf) X(3, kFormIfIf)
 
+bool wavepersist_defer_built(int lds_mode, int form) {
+#define MM_WP(L, F) if (lds_mode == L && form == F) return true;
+    MM_DEFER_INSTANCES(MM_WP)
+#undef MM_WP
+    return false;
+}
+
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s) {
-#define MM_WP(L, F) \
-    if (lds_mode == L && form == F) return launch_wavepersist_t<L, F>(sc, job, samples, stats, err, work, count_stats, s);
+    const bool defer = job.defer_from < (1u << 30);
+#define MM_WP(L, F)                                                                                          \
+    if (lds_mode == L && form == F && defer)                                                                 \
+        return launch_wavepersist_t<L, F, true>(sc, job, samples, stats, err, work, count_stats, s);
+    MM_DEFER_INSTANCES(MM_WP)
+#undef MM_WP
+#define MM_WP(L, F)                                                                                          \
+    if (lds_mode == L && form == F && !defer)                                                                \
+        return launch_wavepersist_t<L, F, false>(sc, job, samples, stats, err, work, count_stats, s);
     MM_WP_INSTANCES(MM_WP)
 #undef MM_WP
     return hipErrorInvalidValue;
@@ -473,7 +497,7 @@ hipError_t launch_trace_tail(const DevScene& sc, const TileJob& job, float4* sam
                              uint32_t* err, bool count_stats, int lds_mode, int form, hipStream_t s) {
 #define MM_WP(L, F) \
     if (lds_mode == L && form == F) return launch_tail_t<L, F>(sc, job, samples, stats, err, count_stats, s);
-    MM_WP_INSTANCES(MM_WP)
+    MM_DEFER_INSTANCES(MM_WP)
 #undef MM_WP
     return hipErrorInvalidValue;
 }
@@ -531,9 +555,26 @@ __global__ void k_resolve(TileJob job, const float4* __restrict__ samples, float
     }
 }
 
+// The same reduction when 64 % spp == 0, a wave per 64 consecutive samples
+// (64/spp whole pixels): every load is one coalesced 1-KB wave access, and
+// resolve_in_wave adds in k_resolve's order (bit-identical).
+__global__ __launch_bounds__(256) void k_resolve_wave(TileJob job, const float4* __restrict__ samples,
+                                                      float4* __restrict__ out) {
+    const uint32_t n = job.w * job.h * job.e.spp;
+    const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;  // waves never straddle the end: n % 64 == 0
+    const bool valid = path < n;                                   // unless the tile is ragged
+    const float4 v = valid ? samples[path] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    resolve_in_wave(job, F3{v.x, v.y, v.z}, path, valid, out);
+}
+
 hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s) {
     const uint32_t n = job.w * job.h;
-    hipLaunchKernelGGL(k_resolve, dim3((n + 255) / 256), dim3(256), 0, s, job, samples, out);
+    if (64 % job.e.spp == 0) {
+        const uint32_t paths = n * job.e.spp;
+        hipLaunchKernelGGL(k_resolve_wave, dim3((paths + 255) / 256), dim3(256), 0, s, job, samples, out);
+    } else {
+        hipLaunchKernelGGL(k_resolve, dim3((n + 255) / 256), dim3(256), 0, s, job, samples, out);
+    }
     return hipGetLastError();
 }
 

@@ -31,6 +31,7 @@ VARIANTS = {
     "bvh-li-split": (1, {7: 5, 9: 80}),
     "mega-lds": (1, {3: 0, 1: 1}),
     "nofuse": (1, {12: 0}),
+    "nodefer": (1, {21: 0}),
     "defer8": (1, {21: 8}),
     "defer16": (1, {21: 16}),
     "defer32": (1, {21: 32}),
