@@ -115,7 +115,7 @@ PIPES = {
     "auto": (0, {}, False),                                  # grid search (C3 default)
     "grid": (1, {7: 11}, False),
     "grid-nofuse": (1, {7: 11, 12: 0}, False),
-    "grid-defer16": (1, {21: 16}, False),
+    "grid-nodefer": (1, {21: 0}, False),
     "grid-defer63": (1, {21: 63}, False),
     "bvh-lean-defer32": (1, {7: 7, 21: 32}, True),
     "bvh-lean-ldsrects": (1, {7: 7}, True),
@@ -173,7 +173,7 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
     ren.close()
 
 
-@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-defer16", "bvh-lean-ldsrects", "bvh-li-dict",
+@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-nodefer", "bvh-lean-ldsrects", "bvh-li-dict",
                                   "mega-lds", "wavefront"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
@@ -218,7 +218,7 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 16}])
+@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 0}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole
@@ -257,10 +257,16 @@ def test_multi_frame_launch_errors(gpu):
     u = default_uniform(64, 64, 0)
     with pytest.raises(MMError):  # frames of one launch cannot accumulate
         r.trace_tile_frames(u, make_ext(8, 3, 15, flags=MM_EXT_ACCUMULATE), 2, 0, 0, 64, 64)
-    with pytest.raises(MMError):  # 3 spp: no fused resolve
-        r.trace_tile_frames(u, make_ext(3, 3, 15), 2, 0, 0, 64, 64)
     with pytest.raises(MMError):
         r.trace_tile_frames(u, make_ext(8, 3, 15), 0, 0, 0, 64, 64)
+    # 3 spp: no fused resolve; with tail deferral (default) the frames are staged and resolved per frame
+    three, _ = r.trace_tile_frames(u, make_ext(3, 3, 15, frame=1), 2, 0, 0, 64, 64)
+    for f in range(2):
+        ref, _ = r.trace_tile(u, make_ext(3, 3, 15, frame=1 + f), 0, 0, 64, 64)
+        assert np.array_equal(_bits(three[f].cpu().numpy()), _bits(ref.cpu().numpy()))
+    r.set_option(21, 0)  # without deferral: needs the fused resolve
+    with pytest.raises(MMError):
+        r.trace_tile_frames(u, make_ext(3, 3, 15), 2, 0, 0, 64, 64)
     one, _ = r.trace_tile_frames(u, make_ext(8, 3, 15, frame=4), 1, 0, 0, 64, 64)
     ref, _ = r.trace_tile(u, make_ext(8, 3, 15, frame=4), 0, 0, 64, 64)
     assert np.array_equal(_bits(one[0].cpu().numpy()), _bits(ref.cpu().numpy()))
@@ -294,12 +300,13 @@ def test_c4_eight_way_row_split_invariance(ren, gpu):
     assert rays == st.rays and st.paths == W * H * 16
 
 
-@pytest.mark.parametrize("fuse", [1, 0])
-def test_accumulate_flag(ren, gpu, fuse):
+@pytest.mark.parametrize("fuse,defer", [(1, 0), (0, 0), (1, 16)])
+def test_accumulate_flag(ren, gpu, fuse, defer):
     from mirror_maze import MM_EXT_ACCUMULATE, default_uniform, make_ext
 
     ren.upload_scene(_scene(10))
     ren.set_option(12, fuse)
+    ren.set_option(21, defer)
     u = default_uniform(128, 96, 0)
     a, _ = ren.trace_tile(u, make_ext(4, 3, 15, frame=0), 0, 0, 128, 96)
     b, _ = ren.trace_tile(u, make_ext(4, 3, 15, frame=1), 0, 0, 128, 96)
