@@ -242,8 +242,7 @@ def main():
     # renderer contexts on their own streams so frame k+1's blocks fill the
     # CUs frame k's tail leaves idle (two frames sharing the GPU run ~7 %
     # slower, profiles/r01_overlap_probe.txt; --contexts 0 times both).
-    n_ctx = (1 if args.accumulate or (args.batch > 1 and args.pipeline != "wave" and 64 % spp == 0)
-             else (args.contexts if args.contexts > 0 else 2))
+    n_ctx = (1 if args.accumulate or args.batch > 1 else (args.contexts if args.contexts > 0 else 2))
     rens = []
     for _ in range(n_ctx):
         r = Renderer(local)
@@ -266,7 +265,8 @@ def main():
     # one RCCL gather per frame, issued async on the frame's stream into
     # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
     # multi-frame launches need the wave-persistent kernel's fused resolve (64 % spp == 0)
-    batchable = not args.accumulate and args.pipeline != "wave" and 64 % spp == 0
+    # (with the mirror-tail deferral -- the default -- samples are staged per frame, any spp)
+    batchable = not args.accumulate
     fb_max = (args.batch if args.batch > 0 else 8) if batchable else 1
     # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,
     # so the next launch never waits on this batch's own gathers

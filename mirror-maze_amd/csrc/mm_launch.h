@@ -92,35 +92,6 @@ bool wavepersist_defer_built(int lds_mode, int form);
 hipError_t launch_trace_tail(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
                              uint32_t* err, bool count_stats, int lds_mode, int form, hipStream_t s);
 
-// ---- wavefront pipeline (trace_wave.hip) ---------------------------------------
-struct WaveState {
-    // SoA path state, indexed by path id (capacity entries each)
-    float* ox; float* oy; float* oz;
-    float* dx; float* dy; float* dz;
-    float* tr; float* tg; float* tb;    // throughput T
-    float* lr; float* lg; float* lb;    // radiance L
-    uint32_t* seed;
-    uint32_t* nm;                       // n | mirror_hits << 16
-    float* hit_t;
-    uint32_t* hit_i;
-    uint32_t* queue[2];                 // live path ids (ping / pong)
-    uint32_t* counters;                 // [0], [1]: queue lengths
-    uint32_t capacity;
-};
-
-struct WaveOpts {
-    bool lds_nodes = true;
-    uint32_t block = 512;               // extend kernel
-    uint32_t extend_blocks = 2048;      // grid cap (grid-stride over the queue)
-};
-
-hipError_t launch_wf_generate(const TileJob& job, const WaveState& ws, float4* samples, hipStream_t s);
-hipError_t launch_wf_extend(const DevScene& sc, const WaveState& ws, int q, uint32_t n_upper,
-                            unsigned long long* stats, bool count_stats, const WaveOpts& o, hipStream_t s);
-hipError_t launch_wf_shade(const DevScene& sc, const TileJob& job, const WaveState& ws, int q, uint32_t n_upper,
-                           float4* samples, unsigned long long* stats, uint32_t* err, bool count_stats,
-                           hipStream_t s);
-
 // Display stage (display.hip).
 hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H, hipStream_t s);
 hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,

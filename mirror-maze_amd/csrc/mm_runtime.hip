@@ -77,9 +77,6 @@ struct mm_ctx {
     // per-sample staging (throughput mode)
     float4* d_samples = nullptr;
     size_t samples_cap = 0;
-    // wavefront SoA state (MM_PIPE_WAVEFRONT)
-    void* d_wave = nullptr;
-    size_t wave_cap = 0;      // paths
     // mirror-tail queue (MM_OPT_DEFER)
     void* d_tail = nullptr;
     uint32_t tail_cap = 0;
@@ -201,32 +198,6 @@ bool extent_ok(float x) {
     return a == 0.0f || (a >= 0x1p-10f && a <= 0x1p60f);
 }
 
-// Carve the wavefront SoA buffers for `n` paths out of one allocation.
-int wave_state(mm_ctx* c, uint32_t n, WaveState& ws) {
-    const size_t n4 = ((size_t)n + 63) & ~(size_t)63;  // 256-B aligned arrays
-    const size_t words = 16 * n4 + 2 * n4 + 64;
-    if (c->wave_cap < n || !c->d_wave) {
-        (void)hipFree(c->d_wave);
-        c->d_wave = nullptr;
-        c->wave_cap = 0;
-        HIPC(c, hipMalloc(&c->d_wave, words * 4));
-        c->wave_cap = n;
-    }
-    const size_t cap4 = (((size_t)c->wave_cap) + 63) & ~(size_t)63;
-    float* f = reinterpret_cast<float*>(c->d_wave);
-    uint32_t* u = reinterpret_cast<uint32_t*>(c->d_wave);
-    ws.ox = f + 0 * cap4; ws.oy = f + 1 * cap4; ws.oz = f + 2 * cap4;
-    ws.dx = f + 3 * cap4; ws.dy = f + 4 * cap4; ws.dz = f + 5 * cap4;
-    ws.tr = f + 6 * cap4; ws.tg = f + 7 * cap4; ws.tb = f + 8 * cap4;
-    ws.lr = f + 9 * cap4; ws.lg = f + 10 * cap4; ws.lb = f + 11 * cap4;
-    ws.seed = u + 12 * cap4; ws.nm = u + 13 * cap4;
-    ws.hit_t = f + 14 * cap4; ws.hit_i = u + 15 * cap4;
-    ws.queue[0] = u + 16 * cap4; ws.queue[1] = u + 17 * cap4;
-    ws.counters = u + 18 * cap4;
-    ws.capacity = c->wave_cap;
-    return MM_OK;
-}
-
 // The mirror-tail queue (mm_launch.h TailQueue): 15 SoA arrays of `cap`
 // entries + 3 counters, one allocation; the counters start at zero and the
 // tail kernel's last wave re-zeroes them.
@@ -325,7 +296,7 @@ void mm_destroy(mm_ctx* c) {
     free_scene(c);
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
-    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_wave); (void)hipFree(c->d_tail);
+    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_tail);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -749,8 +720,9 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     // (32 Mi in the wavefront pipeline).  With the fused resolve there is no
     // staging buffer: one launch covers up to 2^31 paths (a whole C5 frame).
     const uint64_t row_paths = (uint64_t)w * e->spp;
+    // MM_PIPE_WAVEFRONT: the wave-persistent kernel with the compacted mirror-tail queue always on
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
-    const bool persist = !wave && c->pipe != MM_PIPE_REFERENCE && c->opt_persist == 2;
+    const bool persist = c->pipe != MM_PIPE_REFERENCE && (wave || c->opt_persist == 2);
     int form = 0, mode = 0;
     DevScene sc = dev_scene(c);
     if (persist) {
@@ -759,10 +731,10 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     }
     // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run by k_trace_tail; built for
     // the grid search and the lean BVH form with records in LDS (other forms run without it)
-    const bool defer = persist && c->opt_defer > 0 && wavepersist_defer_built(mode, form);
+    const bool defer = persist && (c->opt_defer > 0 || wave) && wavepersist_defer_built(mode, form);
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
     const bool fuse = persist && !defer && c->opt_fuse && 64 % e->spp == 0;
-    const uint64_t batch_paths = (fuse || defer) ? (1ull << 31) : (wave ? (32ull << 20) : (64ull << 20));
+    const uint64_t batch_paths = (fuse || defer) ? (1ull << 31) : (64ull << 20);
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
     if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
@@ -813,31 +785,12 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.reserve_cus = c->opt_reserve_cus;
         if (defer) {
             job.defer_from = 1;
-            job.defer_lanes = (uint32_t)c->opt_defer;
+            job.defer_lanes = c->opt_defer > 0 ? (uint32_t)c->opt_defer : 16u;
             job.tail = tq;
         }
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
-        if (wave) {
-            const uint32_t n = job.w * job.h * job.e.spp;
-            WaveState ws;
-            if ((rc = wave_state(c, n, ws))) return rc;
-            WaveOpts wo;
-            wo.lds_nodes = lds_fits;
-            if (c->opt_block) wo.block = c->opt_block;
-            uint32_t* err = reinterpret_cast<uint32_t*>(c->d_aux + 4);
-            HIPC(c, launch_wf_generate(job, ws, c->d_samples, c->stream));
-            const int max_rays = (int)job.e.bounce_limit + std::max(0, (int)job.e.mirror_limit - 1);
-            for (int it = 0; it < max_rays; ++it) {
-                if ((rc = prof_mark(c))) return rc;
-                HIPC(c, launch_wf_extend(dev_scene(c), ws, it & 1, n, c->d_aux, want_stats, wo, c->stream));
-                if ((rc = prof_mark(c))) return rc;
-                HIPC(c, launch_wf_shade(dev_scene(c), job, ws, it & 1, n, c->d_samples, c->d_aux, err, want_stats,
-                                        c->stream));
-                launches += 2;
-            }
-            launches += 1;
-        } else if (persist) {
+        if (persist) {
             c->last_form = form == kFormGridSlow ? kFormGrid : form;
             c->last_mode = mode;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,

@@ -1,6 +1,8 @@
 #!/bin/bash
-# rocprofv3 summary + PMC passes of the wavefront pipeline (MM_PIPE_WAVEFRONT, trace_wave.hip) on C3, the
-# evidence for retiring it.  One run per counter set, each under its own time limit.
+# rocprofv3 summary + PMC passes of MM_PIPE_WAVEFRONT on C3.  Run at commit 04a553c (before its retirement) it
+# profiled the round-1 flattened pipeline (trace_wave.hip: k_wf_generate/extend/shade), the evidence for
+# retiring it (profiles/r02_wavefront_pmc.txt); MM_PIPE_WAVEFRONT now runs the wave-persistent
+# kernel with the mirror-tail queue.  One run per counter set, each under its own time limit.
 # Usage: bash scripts/pmc_wavefront.sh <tag>
 set -o pipefail
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$1

@@ -129,8 +129,8 @@ PIPES = {
     "bvh-li-dict": (1, {7: 5, 20: 2}, True),
     "bvh-ifif-ldsrects": (1, {7: 0}, True),
     "bvh-ifif-lds": (1, {7: 0, 8: 0}, True),
-    "wavefront": (2, {}, True),
-    "wavefront-global": (2, {1: 0}, True),
+    "wavefront": (2, {}, False),                             # the compacted mirror-tail queue always on
+    "wavefront-global": (2, {1: 0}, False),
 }
 
 
