@@ -97,6 +97,7 @@ struct mm_ctx {
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
     int opt_defer = 16;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
+    uint32_t opt_defer_min = 1u << 21;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
@@ -362,6 +363,10 @@ int mm_set_option(mm_ctx* c, int key, int value) {
         case MM_OPT_DEFER:
             if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "defer lanes must be 0..63");
             c->opt_defer = value;
+            return MM_OK;
+        case MM_OPT_DEFER_MIN:
+            if (value < 0) return fail(c, MM_ERR_INVALID, "defer min paths must be >= 0");
+            c->opt_defer_min = (uint32_t)value;
             return MM_OK;
         case MM_OPT_DICT_NODES:
             if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
@@ -731,7 +736,8 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     }
     // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run by k_trace_tail; built for
     // the grid search and the lean BVH form with records in LDS (other forms run without it)
-    const bool defer = persist && (c->opt_defer > 0 || wave) && wavepersist_defer_built(mode, form);
+    const bool defer = persist && (c->opt_defer > 0 || wave) && wavepersist_defer_built(mode, form) &&
+                       (wave || (uint64_t)w * h * e->spp * n_frames >= c->opt_defer_min);
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
     const bool fuse = persist && !defer && c->opt_fuse && 64 % e->spp == 0;
     const uint64_t batch_paths = (fuse || defer) ? (1ull << 31) : (64ull << 20);

@@ -100,7 +100,7 @@ def test_c4_rank0_of_eight_way_split(gpu):
 C5_WINDOWS = [(0, 0), (1904, 1064), (3808, 2144), (700, 1500), (2900, 300), (1200, 40)]
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 7}], ids=["auto", "bvh-lean-dict"])
+@pytest.mark.parametrize("opts", [{}, {22: 0}, {7: 7}], ids=["auto", "auto-tail-deferral", "bvh-lean-dict"])
 def test_c5_windows_64spp(gpu, opts):
     """C5: 64x64 maze, 3840x2160 frame coordinates, 64 spp, 16/16 bounces --
     the reference's 64-sample reduction (shaders.metal:342-364) as the fused

@@ -116,8 +116,9 @@ PIPES = {
     "grid": (1, {7: 11}, False),
     "grid-nofuse": (1, {7: 11, 12: 0}, False),
     "grid-nodefer": (1, {21: 0}, False),
-    "grid-defer63": (1, {21: 63}, False),
-    "bvh-lean-defer32": (1, {7: 7, 21: 32}, True),
+    "grid-defer16": (1, {22: 0}, False),                     # tail deferral on any launch size
+    "grid-defer63": (1, {21: 63, 22: 0}, False),
+    "bvh-lean-defer32": (1, {7: 7, 21: 32, 22: 0}, True),
     "bvh-lean-ldsrects": (1, {7: 7}, True),
     "bvh-lean-globalrecs": (1, {7: 7, 8: 0}, True),
     "bvh-lean-split2kb": (1, {7: 7, 9: 2}, True),
@@ -173,8 +174,8 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
     ren.close()
 
 
-@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-nodefer", "bvh-lean-ldsrects", "bvh-li-dict",
-                                  "mega-lds", "wavefront"])
+@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-nodefer", "grid-defer16", "bvh-lean-ldsrects",
+                                  "bvh-li-dict", "mega-lds", "wavefront"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -218,7 +219,7 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 0}])
+@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 0}, {22: 0}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole
@@ -259,7 +260,8 @@ def test_multi_frame_launch_errors(gpu):
         r.trace_tile_frames(u, make_ext(8, 3, 15, flags=MM_EXT_ACCUMULATE), 2, 0, 0, 64, 64)
     with pytest.raises(MMError):
         r.trace_tile_frames(u, make_ext(8, 3, 15), 0, 0, 0, 64, 64)
-    # 3 spp: no fused resolve; with tail deferral (default) the frames are staged and resolved per frame
+    # 3 spp: no fused resolve; with tail deferral the frames are staged and resolved per frame
+    r.set_option(22, 0)
     three, _ = r.trace_tile_frames(u, make_ext(3, 3, 15, frame=1), 2, 0, 0, 64, 64)
     for f in range(2):
         ref, _ = r.trace_tile(u, make_ext(3, 3, 15, frame=1 + f), 0, 0, 64, 64)
@@ -300,13 +302,13 @@ def test_c4_eight_way_row_split_invariance(ren, gpu):
     assert rays == st.rays and st.paths == W * H * 16
 
 
-@pytest.mark.parametrize("fuse,defer", [(1, 0), (0, 0), (1, 16)])
-def test_accumulate_flag(ren, gpu, fuse, defer):
+@pytest.mark.parametrize("fuse,defer_min", [(1, 1 << 30), (0, 1 << 30), (1, 0), (1, 1 << 21)])
+def test_accumulate_flag(ren, gpu, fuse, defer_min):
     from mirror_maze import MM_EXT_ACCUMULATE, default_uniform, make_ext
 
     ren.upload_scene(_scene(10))
     ren.set_option(12, fuse)
-    ren.set_option(21, defer)
+    ren.set_option(22, defer_min)
     u = default_uniform(128, 96, 0)
     a, _ = ren.trace_tile(u, make_ext(4, 3, 15, frame=0), 0, 0, 128, 96)
     b, _ = ren.trace_tile(u, make_ext(4, 3, 15, frame=1), 0, 0, 128, 96)
