@@ -13,9 +13,9 @@
 // (SKIP records: never hit) go nowhere.  Rects that are not axis-aligned
 // with exact unit normals (SLOW records) are listed too; the kernel runs the
 // general ray_rect_intersect on them (grid_rect<kSlow>).
-// Per rect the image also holds its compact record (rect_compact.cpp, built
-// with identity slots) and the box of the reference BVH leaf holding it --
-// the box the certificate tests.
+// Per rect the image also holds its grid record (mm_grid.h: grid_rect; made
+// from rect_compact.cpp's record, built with identity slots) and the box of
+// the reference BVH leaf holding it -- the box the certificate tests.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -23,22 +23,13 @@
 #include <string>
 #include <vector>
 
+#include "grid_build.h"
 #include "mm_types.h"
 
 namespace mm {
 
 size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
                            size_t* n_slow);
-
-struct GridHost {
-    float mn[3], mx[3], cell[3], inv[3];
-    int n[3];
-    uint32_t n_glob = 0;
-    uint32_t glob[4] = {0, 0, 0, 0};
-    uint32_t off_list = 0, off_recs = 0, off_box = 0, bytes = 0;
-    uint32_t n_list = 0;
-    std::vector<uint8_t> image;
-};
 
 namespace {
 
@@ -52,6 +43,80 @@ void rect_box(const mm_rect& r, double lo[3], double hi[3]) {
 }
 
 inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+inline uint32_t f2u(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+inline float u2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+inline int64_t fkey(float f) {  // monotone integer key of a non-NaN float (+-0 -> 0)
+    const uint32_t u = f2u(f);
+    return (u & 0x80000000u) ? -(int64_t)(u & 0x7FFFFFFFu) : (int64_t)u;
+}
+inline float from_key(int64_t k) { return k >= 0 ? u2f((uint32_t)k) : u2f(0x80000000u | (uint32_t)(-k)); }
+inline float mul_rn(float x, float s) {
+    volatile float a = x, b = s;
+    return a * b;
+}
+
+// {Y : xlo <= RN(Y * s) <= xhi} for the compact record's X thresholds.  Y ->
+// RN(Y * s) is monotone, so the set is an interval of floats; it holds 0
+// (xlo <= 0 <= xhi, checked) and not +-inf (finite thresholds), and its ends
+// are found by bisection over the float order.  The kernel's test
+// ylo <= Y <= yhi is then the same predicate, bit for bit, for every Y
+// (NaN fails both forms).
+bool fold_thresholds(float s, float xlo, float xhi, float& ylo, float& yhi) {
+    auto P = [&](float y) { const float p = mul_rn(y, s); return p >= xlo && p <= xhi; };
+    if (!std::isfinite(s) || s == 0.0f || !std::isfinite(xlo) || !std::isfinite(xhi) || !P(0.0f) || P(INFINITY) ||
+        P(-INFINITY))
+        return false;
+    int64_t lo = fkey(0.0f), hi = fkey(INFINITY);  // P(lo) true, P(hi) false
+    while (hi - lo > 1) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (P(from_key(mid))) lo = mid; else hi = mid;
+    }
+    yhi = from_key(lo);
+    lo = fkey(-INFINITY); hi = fkey(0.0f);  // P(lo) false, P(hi) true
+    while (hi - lo > 1) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (P(from_key(mid))) hi = mid; else lo = mid;
+    }
+    ylo = from_key(hi);
+    return true;
+}
+
+// rect_compact.cpp's 10-word record of each rect -> the 8-word grid record
+// (mm_grid.h).  A record whose thresholds do not fold becomes SLOW.
+uint32_t grid_records(const std::vector<uint32_t>& rc, uint32_t n_rects, std::vector<uint32_t>& out) {
+    out.assign(8 * (size_t)n_rects, 0);
+    uint32_t n_slow = 0;
+    for (uint32_t k = 0; k < n_rects; ++k) {
+        const uint32_t* w = &rc[10 * (size_t)k];
+        uint32_t* g = &out[8 * (size_t)k];
+        uint32_t kind = w[9] >> 30;
+        const uint32_t ak = (w[9] >> 20) & 3u, av = (w[9] >> 22) & 3u, au = (w[9] >> 24) & 3u;
+        if (kind == 0u) {
+            float y1lo, y1hi, y2lo, y2hi;
+            if (fold_thresholds(u2f(w[3]), u2f(w[5]), u2f(w[6]), y1lo, y1hi) &&
+                fold_thresholds(u2f(w[4]), u2f(w[7]), u2f(w[8]), y2lo, y2hi)) {
+                const bool swap = av > au;  // the lower axis first
+                g[0] = w[0];
+                g[1] = swap ? w[2] : w[1];
+                g[2] = swap ? w[1] : w[2];
+                g[3] = f2u(swap ? y2lo : y1lo);
+                g[4] = f2u(swap ? y2hi : y1hi);
+                g[5] = f2u(swap ? y1lo : y2lo);
+                g[6] = f2u(swap ? y1hi : y2hi);
+            } else {
+                kind = 2u;
+            }
+        }
+        if (kind == 1u) {  // never hits (not listed either)
+            g[3] = g[5] = f2u(INFINITY);
+            g[4] = g[6] = f2u(-INFINITY);
+        }
+        g[7] = k | ((kind == 0u ? ak : 0u) << 20) | (kind << 30);
+        n_slow += kind == 2u;
+    }
+    return n_slow;
+}
 
 // Cells of size ~s over the scene box widened by eps = C * 2^-14, their lists
 // and the image layout (recs and boxes are filled by the caller).
@@ -124,7 +189,7 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
             if (g.n_list >= (1u << 22)) { why = "more than 2^22 list entries"; return false; }
             g.off_list = align16(4u * (uint32_t)total);
             g.off_recs = align16(g.off_list + 2u * g.n_list);
-            g.off_box = align16(g.off_recs + 40u * n_rects);
+            g.off_box = align16(g.off_recs + 32u * n_rects);
             g.bytes = align16(g.off_box + 24u * n_rects);
             g.image.assign(g.bytes, 0);
             for (long c = 0; c < total; ++c) {
@@ -175,7 +240,9 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
             break;
         if (attempt == 23) { why = "no grid index fits the LDS budget"; return false; }
     }
-    std::memcpy(&g.image[g.off_recs], recs.data(), 40u * (size_t)n_rects);
+    std::vector<uint32_t> grecs;
+    g.n_slow = grid_records(recs, n_rects, grecs);
+    std::memcpy(&g.image[g.off_recs], grecs.data(), 32u * (size_t)n_rects);
     // the reference leaf box of every rect; a rect in no leaf gets an empty
     // box, so a certificate for it always fails (the reference never tests it)
     std::vector<float> box(6 * (size_t)n_rects);

@@ -1,0 +1,29 @@
+// grid_build.h — host side of the certified grid search: the grid image
+// (mm_device.h: DevGrid) built from the scene and its reference BVH.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mm_types.h"
+
+namespace mm {
+
+struct GridHost {
+    float mn[3], mx[3], cell[3], inv[3];
+    int n[3];
+    uint32_t n_glob = 0;
+    uint32_t glob[4] = {0, 0, 0, 0};
+    uint32_t off_list = 0, off_recs = 0, off_box = 0, bytes = 0;
+    uint32_t n_list = 0;
+    uint32_t n_slow = 0;  // records the kernel tests with the general statement
+    std::vector<uint8_t> image;
+};
+
+// Returns false (with a reason) when the scene does not suit the search.
+bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
+                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why);
+
+}  // namespace mm

@@ -37,8 +37,9 @@ enum : int { kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7, kFormGrid = 11
 // Shade record: s0 = (color.rgb, is_mirror), s1 = emission (rgba).
 // Uniform grid of the certified search (mm_grid.h, built by grid_build.cpp).
 // The device image is one buffer: [cells: n_cells u32][list: u16, padded to
-// 16 B][recs: 5 x uint2 per rect][box: 3 x float2 per rect]; the byte
-// offsets of the sections let a kernel stage a prefix of it in LDS.
+// 16 B][recs: 2 x uint4 per rect][box: 3 x float2 per rect]; the byte
+// offsets of the sections let a kernel stage it in LDS (all of it, records
+// first, or the cells + lists prefix).
 struct DevGrid {
     float mn[3], mx[3];        // grid box (scene bounds widened by eps)
     float cell[3], inv[3];     // cell size per axis and its reciprocal
@@ -47,7 +48,7 @@ struct DevGrid {
     uint32_t glob[4];
     const uint32_t* cells;     // per cell: first list entry | count << 22
     const uint16_t* list;      // rect indices
-    const uint2* recs;         // per-rect compact records (rect_compact.cpp, FAST)
+    const uint4* recs;         // per-rect grid records (grid_build.cpp; mm_grid.h: grid_rect)
     const float2* box;         // per rect: its reference leaf's box, (mn, mx) per axis
     const uint4* image;        // the whole image (16-B units)
     uint32_t off_list, off_recs, off_box, bytes;  // section offsets in bytes

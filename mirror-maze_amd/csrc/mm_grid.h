@@ -69,26 +69,36 @@ __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo
     if (d1 >= 0.0f && d1 <= lv && d2 >= 0.0f && d2 <= lu && nc != 0.0f && a > 0.1f) grid_update(a, k, best, bk, tie);
 }
 
+// Grid records (grid_build.cpp, 8 x u32 per rect, indexed by rect):
+//   0 o_k  1 o_v  2 o_u  3 Yv_lo  4 Yv_hi  5 Yu_lo  6 Yu_hi  7 k | k_axis << 20 | kind << 30
+// v = the lower of the two in-plane axes, u = the higher (so both follow from
+// k_axis), and the compact record's test X_lo <= RN(Y * v_axis) <= X_hi folded
+// into thresholds on Y = (ori_v - o_v) + a * d_v itself.
+__device__ __forceinline__ float sel_k(bool k0, bool k2, F3 v) { return k0 ? v.x : (k2 ? v.z : v.y); }
+
 template <bool kSlow, typename R>
 __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restrict__ geo, uint32_t k, const Ray& r,
                                           float& best, uint32_t& bk, bool& tie) {
-    const uint2 w01 = recs[5 * k + 0], w23 = recs[5 * k + 1], w45 = recs[5 * k + 2], w67 = recs[5 * k + 3],
-                w89 = recs[5 * k + 4];
-    const uint32_t meta = w89.y;
+    const uint4 w0 = recs[2 * k + 0], w1 = recs[2 * k + 1];
+    const uint32_t meta = w1.w;
     if constexpr (kSlow) {
         if ((meta >> 30) == 2u) {
             grid_rect_general(geo, k, r, best, bk, tie);
             return;
         }
     }
-    const uint32_t ak = (meta >> 20) & 3u, av = (meta >> 22) & 3u, au = (meta >> 24) & 3u;
-    const float a = qdiv(__uint_as_float(w01.x) - sel3(ak, r.o), sel3(ak, r.d), sel3(ak, r.y));
-    const float x1 = ((sel3(av, r.o) - __uint_as_float(w01.y)) + a * sel3(av, r.d)) * __uint_as_float(w23.y);
-    const float x2 = ((sel3(au, r.o) - __uint_as_float(w23.x)) + a * sel3(au, r.d)) * __uint_as_float(w45.x);
+    const uint32_t ak = (meta >> 20) & 3u;
+    const bool k0 = ak == 0u, k2 = ak == 2u;
+    const float ok = sel_k(k0, k2, r.o), dk = sel_k(k0, k2, r.d), yk = sel_k(k0, k2, r.y);
+    const float ov = k0 ? r.o.y : r.o.x, dv = k0 ? r.d.y : r.d.x;
+    const float ou = k2 ? r.o.y : r.o.z, du = k2 ? r.d.y : r.d.z;
+    const float a = qdiv(__uint_as_float(w0.x) - ok, dk, yk);
+    const float y1 = (ov - __uint_as_float(w0.y)) + a * dv;
+    const float y2 = (ou - __uint_as_float(w0.z)) + a * du;
     // (a branch-free update measured 6.11 vs 5.86 ms on C3: most tests miss,
     // and the branch skips the update for the whole wave)
-    if (x1 >= __uint_as_float(w45.y) && x1 <= __uint_as_float(w67.x) && x2 >= __uint_as_float(w67.y) &&
-        x2 <= __uint_as_float(w89.x) && a > 0.1f)
+    if (y1 >= __uint_as_float(w0.w) && y1 <= __uint_as_float(w1.x) && y2 >= __uint_as_float(w1.y) &&
+        y2 <= __uint_as_float(w1.z) && a > 0.1f)
         grid_update(a, k, best, bk, tie);
 }
 
@@ -97,7 +107,7 @@ template <typename CellsT, typename ListT, typename RecsT, typename BoxT>
 struct GridView {
     CellsT cells;  // per cell: first list entry | count << 22
     ListT list;    // rect indices (u16)
-    RecsT recs;    // 5 x uint2 per rect
+    RecsT recs;    // 2 x uint4 per rect
     BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
 };
 template <typename C, typename L, typename R, typename B>

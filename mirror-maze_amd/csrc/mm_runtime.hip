@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "grid_build.h"
 #include "mm_api.h"
 #include "mm_launch.h"
 
@@ -23,17 +24,6 @@ using namespace mm;
 namespace mm {
 size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
                            size_t* n_slow);
-struct GridHost {
-    float mn[3], mx[3], cell[3], inv[3];
-    int n[3];
-    uint32_t n_glob = 0;
-    uint32_t glob[4] = {0, 0, 0, 0};
-    uint32_t off_list = 0, off_recs = 0, off_box = 0, bytes = 0;
-    uint32_t n_list = 0;
-    std::vector<uint8_t> image;
-};
-bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
-                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why);
 }
 
 struct mm_ctx {
@@ -59,6 +49,7 @@ struct mm_ctx {
     uint8_t* d_grid = nullptr;  // certified grid search (grid_build.cpp, mm_grid.h)
     DevGrid grid{};
     bool grid_ok = false;
+    bool grid_slow = false;  // the grid has SLOW records (general rect test)
     std::string grid_why;
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
@@ -152,7 +143,7 @@ void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_nodes_ref); (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
     (void)hipFree(c->d_grid);
-    c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false;
+    c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false; c->grid_slow = false;
     (void)hipFree(c->d_dict_tab); (void)hipFree(c->d_dict_words);
     c->d_dict_tab = nullptr; c->d_dict_words = nullptr; c->dict_ok = false;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
@@ -522,10 +513,11 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         for (int i = 0; i < 4; ++i) dg.glob[i] = gh.glob[i];
         dg.cells = reinterpret_cast<const uint32_t*>(c->d_grid);
         dg.list = reinterpret_cast<const uint16_t*>(c->d_grid + gh.off_list);
-        dg.recs = reinterpret_cast<const uint2*>(c->d_grid + gh.off_recs);
+        dg.recs = reinterpret_cast<const uint4*>(c->d_grid + gh.off_recs);
         dg.box = reinterpret_cast<const float2*>(c->d_grid + gh.off_box);
         dg.image = reinterpret_cast<const uint4*>(c->d_grid);
         dg.off_list = gh.off_list; dg.off_recs = gh.off_recs; dg.off_box = gh.off_box; dg.bytes = gh.bytes;
+        c->grid_slow = gh.n_slow > 0;
     }
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     if (dict_ok) {
@@ -665,7 +657,7 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
     if (form == kFormGrid) {
         if (!c->grid_ok)
             return fail(c, MM_ERR_UNSUPPORTED, "grid search unavailable for this scene: " + c->grid_why);
-        if (!c->lean_ok) form = kFormGridSlow;  // general rect tests for the SLOW records
+        if (!c->lean_ok || c->grid_slow) form = kFormGridSlow;  // general rect tests for the SLOW records
         if (c->opt_lds && c->grid.bytes <= budget) { mode = 11; return MM_OK; }
         if (c->opt_lds && c->grid.off_recs <= budget) { mode = 12; return MM_OK; }
         if (!auto_form || !c->opt_lds) { mode = 13; return MM_OK; }

@@ -298,23 +298,34 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
             if (wid < job.wave_ts_cap) job.wave_ts[4 * wid + 1] = (unsigned long long)wall_clock64();
         }
     };
-    if constexpr (kLds == 11 || kLds == 12) {
-        const uint32_t n16 = (kLds == 11 ? sc.grid.bytes : sc.grid.off_recs) / 16u;
+    if constexpr (kLds == 11) {
+        // records + boxes first, at LDS address 0 (a constant in the rect test),
+        // then cells + lists
+        const uint32_t nr16 = (sc.grid.bytes - sc.grid.off_recs) / 16u, ni16 = sc.grid.off_recs / 16u;
+        uint4* img = reinterpret_cast<uint4*>(lds);
+        const uint4* src = sc.grid.image;
+        for (uint32_t i = threadIdx.x; i < nr16; i += blockDim.x) img[i] = src[ni16 + i];
+        for (uint32_t i = threadIdx.x; i < ni16; i += blockDim.x) img[nr16 + i] = src[i];
+        __syncthreads();
+        staged();
+        const char* base = reinterpret_cast<const char*>(lds);
+        const char* index = base + 16u * nr16;
+        const auto gv = grid_view(reinterpret_cast<const uint32_t*>(index),
+                                  reinterpret_cast<const uint16_t*>(index + sc.grid.off_list),
+                                  reinterpret_cast<const uint4*>(lds),
+                                  reinterpret_cast<const float2*>(base + (sc.grid.off_box - sc.grid.off_recs)));
+        return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
+    } else if constexpr (kLds == 12) {
+        const uint32_t n16 = sc.grid.off_recs / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
         for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) img[i] = sc.grid.image[i];
         __syncthreads();
         staged();
         const char* base = reinterpret_cast<const char*>(lds);
-        const uint32_t* cells = reinterpret_cast<const uint32_t*>(base);
-        const uint16_t* list = reinterpret_cast<const uint16_t*>(base + sc.grid.off_list);
-        if constexpr (kLds == 11) {
-            const auto gv = grid_view(cells, list, reinterpret_cast<const uint2*>(base + sc.grid.off_recs),
-                                      reinterpret_cast<const float2*>(base + sc.grid.off_box));
-            return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
-        } else {
-            const auto gv = grid_view(cells, list, sc.grid.recs, sc.grid.box);
-            return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
-        }
+        const auto gv = grid_view(reinterpret_cast<const uint32_t*>(base),
+                                  reinterpret_cast<const uint16_t*>(base + sc.grid.off_list), sc.grid.recs,
+                                  sc.grid.box);
+        return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 13) {
         const auto gv = grid_view(sc.grid.cells, sc.grid.list, sc.grid.recs, sc.grid.box);
         return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
