@@ -46,18 +46,25 @@ namespace mm {
 // a < t).  Records are rect_compact.cpp's FAST records, indexed by rect.
 // With kSlow, SLOW records (rects without an exact axis-aligned form) run the
 // general statement on the rect geometry (rect_test's operations).
-__device__ __forceinline__ void grid_update(float a, uint32_t k, float& best, uint32_t& bk, bool& tie) {
+__device__ __forceinline__ void grid_update(float a, uint32_t k, float& best, uint32_t& bk, uint32_t& tie) {
     if (a < best) {
         best = a;
         bk = k;
-        tie = false;
+        tie = 0u;
     } else if (a == best && k != bk) {
-        tie = true;
+        tie = 1u;
     }
 }
 
+__device__ __forceinline__ void grid_update_sel(float a, uint32_t k, float& best, uint32_t& bk, uint32_t& tie) {
+    const bool lt = a < best, eq = (a == best) & (k != bk);
+    tie = lt ? 0u : (tie | (eq ? 1u : 0u));
+    bk = lt ? k : bk;
+    best = lt ? a : best;
+}
+
 __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo, uint32_t k, const Ray& r,
-                                                  float& best, uint32_t& bk, bool& tie) {
+                                                  float& best, uint32_t& bk, uint32_t& tie) {
     const float4 g0 = geo[4 * k + 0], g1 = geo[4 * k + 1], g2 = geo[4 * k + 2], g3 = geo[4 * k + 3];
     const F3 o = xyz(g0), n = xyz(g1), v = xyz(g2), u = xyz(g3);
     const float lv = g0.w, lu = g1.w;
@@ -75,10 +82,11 @@ __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo
 // k_axis), and the compact record's test X_lo <= RN(Y * v_axis) <= X_hi folded
 // into thresholds on Y = (ori_v - o_v) + a * d_v itself.
 __device__ __forceinline__ float sel_k(bool k0, bool k2, F3 v) { return k0 ? v.x : (k2 ? v.z : v.y); }
+__device__ __forceinline__ float sel_xy(bool sx, bool sy, F3 v) { return sx ? v.x : (sy ? v.y : v.z); }
 
 template <bool kSlow, typename R>
 __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restrict__ geo, uint32_t k, const Ray& r,
-                                          float& best, uint32_t& bk, bool& tie) {
+                                          float& best, uint32_t& bk, uint32_t& tie) {
     const uint4 w0 = recs[2 * k + 0], w1 = recs[2 * k + 1];
     const uint32_t meta = w1.w;
     if constexpr (kSlow) {
@@ -95,11 +103,13 @@ __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restric
     const float a = qdiv(__uint_as_float(w0.x) - ok, dk, yk);
     const float y1 = (ov - __uint_as_float(w0.y)) + a * dv;
     const float y2 = (ou - __uint_as_float(w0.z)) + a * du;
-    // (a branch-free update measured 6.11 vs 5.86 ms on C3: most tests miss,
-    // and the branch skips the update for the whole wave)
-    if (y1 >= __uint_as_float(w0.w) && y1 <= __uint_as_float(w1.x) && y2 >= __uint_as_float(w1.y) &&
-        y2 <= __uint_as_float(w1.z) && a > 0.1f)
-        grid_update(a, k, best, bk, tie);
+    // One branch around a select-form update (a branch-free update measured
+    // 6.11 vs 5.86 ms on C3: most tests miss, and the branch skips the update
+    // for the whole wave; && chains compile to one exec-mask branch per clause).
+    const uint32_t hit = (uint32_t)(y1 >= __uint_as_float(w0.w)) & (uint32_t)(y1 <= __uint_as_float(w1.x)) &
+                         (uint32_t)(y2 >= __uint_as_float(w1.y)) & (uint32_t)(y2 <= __uint_as_float(w1.z)) &
+                         (uint32_t)(a > 0.1f);
+    if (hit) grid_update_sel(a, k, best, bk, tie);
 }
 
 // Where the grid's arrays are read from (LDS or global memory).
@@ -146,7 +156,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
                                             const Ray& r, float& t, uint32_t& index, Counters& c) {
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
-    bool tie = false;
+    uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
     for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect<kSlow>(gv.recs, geo, g.glob[j], r, best, bk, tie);
     int bx = grid_first(g, 0, r.o.x, r.y.x), by = grid_first(g, 1, r.o.y, r.y.y), bz = grid_first(g, 2, r.o.z, r.y.z);
     float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
@@ -169,19 +179,27 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         if (j >= jend) {
             const float te = fminf(tx, fminf(ty, tz));
             if (best < te) break;
-            if (tx == te) {
-                bx += r.y.x > 0.0f ? 1 : -1;
-                if (bx < 0 || bx > g.n[0]) break;
-                tx = grid_time(g, 0, bx, r.o.x, r.y.x);
-            } else if (ty == te) {
-                by += r.y.y > 0.0f ? 1 : -1;
-                if (by < 0 || by > g.n[1]) break;
-                ty = grid_time(g, 1, by, r.o.y, r.y.y);
-            } else {
-                bz += r.y.z > 0.0f ? 1 : -1;
-                if (bz < 0 || bz > g.n[2]) break;
-                tz = grid_time(g, 2, bz, r.o.z, r.y.z);
-            }
+            // step the axis whose boundary comes first (x before y before z on
+            // equal times) -- in selects: three exec-mask branches here cost
+            // more SALU and SGPR spills than the selects cost VALU
+            const bool sx = tx == te, sy = !sx && ty == te, sz = !sx && !sy;
+            bx += sx ? (r.y.x > 0.0f ? 1 : -1) : 0;
+            by += sy ? (r.y.y > 0.0f ? 1 : -1) : 0;
+            bz += sz ? (r.y.z > 0.0f ? 1 : -1) : 0;
+            if (((uint32_t)bx > (uint32_t)g.n[0]) | ((uint32_t)by > (uint32_t)g.n[1]) |
+                ((uint32_t)bz > (uint32_t)g.n[2]))
+                break;
+            // grid_time of the stepped axis, the same operations on selected operands
+            // (by-value selects: a select of two loads becomes a load of a
+            // selected address -- of the kernel argument or a scratch copy)
+            const int b = sx ? bx : (sy ? by : bz);
+            const float mn = sel_xy(sx, sy, F3{g.mn[0], g.mn[1], g.mn[2]});
+            const float cs = sel_xy(sx, sy, F3{g.cell[0], g.cell[1], g.cell[2]});
+            const float oa = sel_xy(sx, sy, r.o), ya = sel_xy(sx, sy, r.y);
+            const float nt = ((mn + (float)b * cs) - oa) * ya;
+            tx = sx ? nt : tx;
+            ty = sy ? nt : ty;
+            tz = sz ? nt : tz;
             cw = cell_word();
             j = cw & 0x3FFFFFu;
             jend = j + (cw >> 22);

@@ -96,6 +96,8 @@ static void build_grid(double cell_target) {
     long total = 1;
     for (int a = 0; a < 3; ++a) {
         double lo = smin[a] - geps, hi = smax[a] + geps;
+        /* SHIFT=f: move the grid origin down by f cells (ALIGN: cells of exactly cell_target) */
+        if (getenv("SHIFT")) lo -= atof(getenv("SHIFT")) * cell_target;
         int n = (int)floor((hi - lo) / cell_target + 0.5);
         if (getenv("ALIGN")) n = (int)ceil((hi - lo) / cell_target);
         if (n < 1) n = 1;
@@ -322,7 +324,7 @@ int main(int argc, char** argv) {
     u.view_w = (float)W; u.view_h = (float)H; u.chunk_w = 4; u.time = 0;
     gstats tot;
     memset(&tot, 0, sizeof tot);
-    double wnest = 0, wflat = 0, wlane = 0, wcont[4] = {0, 0, 0, 0};
+    double wnest = 0, wflat = 0, wlane = 0, wcont[4] = {0, 0, 0, 0}, wtest = 0, wstep = 0, wshade = 0;
     double gnbmax = 0, gnbsum = 0, gnbw = 0, gact[32] = {0}, git[32] = {0};
     uint64_t rays_tot = 0;
 #pragma omp parallel
@@ -331,7 +333,7 @@ int main(int argc, char** argv) {
         memset(&st, 0, sizeof st);
         trav_t tr = {0, 0, 0};
         uint64_t rays = 0;
-        double nest = 0, flat = 0, lanework = 0, ideal = 0, lockS = 0, cont[4] = {0, 0, 0, 0};
+        double nest = 0, flat = 0, lanework = 0, ideal = 0, lockS = 0, cont[4] = {0, 0, 0, 0}, ntest = 0, nstep = 0;
         double nbmax = 0, nbsum = 0, nbw = 0, act_hist[32] = {0}, it_hist[32] = {0};
 #pragma omp for schedule(dynamic, 1)
         for (int y = 0; y < H; y += rs)
@@ -365,6 +367,7 @@ int main(int argc, char** argv) {
                         int mx = 0;
                         for (int l = 0; l < 64; ++l) if (w_nb[l] > b && w_n[l][b] > c && w_len[l][b][c] > mx) mx = w_len[l][b][c];
                         nest += mx * 45.0 + 25.0;
+                        ntest += mx * 45.0; nstep += 25.0;
                     }
                     flat += maxflat * 70.0;
                     lockS += 250.0;
@@ -399,7 +402,7 @@ int main(int argc, char** argv) {
                 }
             }
 #pragma omp critical
-        { wnest += nest + lockS; wflat += flat + lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K];
+        { wnest += nest + lockS; wflat += flat + lockS; wtest += ntest; wstep += nstep; wshade += lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K];
           gnbmax += nbmax; gnbsum += nbsum; gnbw += nbw; for (int b = 0; b < 32; ++b) { gact[b] += act_hist[b]; git[b] += it_hist[b]; } }
 #pragma omp critical
         {
@@ -417,6 +420,7 @@ int main(int argc, char** argv) {
            (unsigned long long)tot.mismatch);
     printf("wave model (VALU slots x64 per wave): nested %.4g  flat %.4g  ideal(lane work/64) %.4g  -> util nested %.3f flat %.3f\n",
            wnest, wflat, wlane / 64, wlane / 64 / wnest, wlane / 64 / wflat);
+    printf("nested split: tests %.4g  cell steps %.4g  shading %.4g\n", wtest, wstep, wshade);
     printf("with shading (250/bounce): lockstep nested %.4g flat %.4g | continuous thr1 %.4g thr16 %.4g thr32 %.4g thr64 %.4g\n",
            wnest, wflat, wcont[0], wcont[1], wcont[2], wcont[3]);
     printf("per wave: mean of max queries/lane %.3f, mean queries/lane %.3f\n", gnbmax / gnbw, gnbsum / gnbw);
