@@ -454,11 +454,17 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
     const F3 nn = xyz(sc.geo[4 * k + 1]);                    // normalize(cross(v,u)), %238
     const float4 s0 = sc.shade[2 * k + 0];                   // color, is_mirror
     const float sg = msign(dot3(p.dir, nn));
-    const float side = -sg;
-    if (s0.w == 0.0f || sg == 1.0f) {
+    const bool diffuse = s0.w == 0.0f || sg == 1.0f;
+    if (!diffuse && !(p.mh + 1 < mirror_limit)) return false;  // shaders.metal:326, 333
+    // Both branches end in ori += t dir, dir = normalize(X), L = contrib + L;
+    // those run once after the branch (a wave holding diffuse and mirror lanes
+    // would otherwise execute the correctly rounded 1/sqrt of each branch).
+    F3 x, contrib;
+    if (diffuse) {
+        const float side = -sg;
         const float4 e = sc.shade[2 * k + 1];
-        const F3 contrib = (e.w * p.T) * xyz(e);             // %253, %254
-        const F3 newT = xyz(s0) * p.T;                       // %264
+        contrib = (e.w * p.T) * xyz(e);                      // %253, %254
+        p.T = xyz(s0) * p.T;                                 // %264
         float rx = rand_pm1(p.seed), ry = rand_pm1(p.seed), rz = rand_pm1(p.seed);
         F3 rd = F3{rx, ry, rz};
         float len2 = dot3(rd, rd);
@@ -470,21 +476,16 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
             len2 = dot3(rd, rd);
         }
         const F3 rn = rsq(len2) * rd;                        // %358
-        p.ori = p.ori + t * p.dir;                           // %363
-        const F3 nd = rn + side * nn;                        // %367
-        p.dir = rsq(dot3(nd, nd)) * nd;                      // %372
-        p.L = contrib + p.L;                                 // %409
-        p.T = newT;
+        x = rn + side * nn;                                  // %367
     } else {
-        if (!(p.mh + 1 < mirror_limit)) return false;        // shaders.metal:326, 333
-        const F3 contrib = 0.005f * xyz(s0);                 // %386
-        p.ori = p.ori + t * p.dir;
+        contrib = 0.005f * xyz(s0);                          // %386
         const float dd = dot3(nn, p.dir) * 2.0f;             // reflect, %392-%397
-        const F3 rf = p.dir - dd * nn;
-        p.dir = rsq(dot3(rf, rf)) * rf;
-        p.L = contrib + p.L;
+        x = p.dir - dd * nn;
         p.mh += 1;
     }
+    p.ori = p.ori + t * p.dir;                               // %363
+    p.dir = rsq(dot3(x, x)) * x;                             // %372 / reflect's normalize
+    p.L = contrib + p.L;                                     // %409
     return true;
 }
 
