@@ -196,7 +196,8 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
  *   MM_INFO_DEPTH            BVH depth (max traversal stack entries)
  *   MM_INFO_DICT_OK          1 if the nodes have <= 256 distinct bound values (dictionary nodes possible)
  *   MM_INFO_LAST_FORM        query method of the last wave-persistent launch (MM_OPT_TRAVERSAL value)
- *   MM_INFO_LAST_LDS_MODE    its LDS mode (trace_kernels.hip: 0, 1, 3, 6, 7, 10 BVH; 11-13 grid) */
+ *   MM_INFO_LAST_LDS_MODE    its LDS mode (trace_kernels.hip: 0, 1, 3, 6, 7, 10 BVH; 11-13 grid)
+ *   MM_INFO_GRID_FACES       1 if the grid cells carry per-face list ranges (64-bit cell words) */
 #define MM_INFO_GRID_OK          1
 #define MM_INFO_GRID_CELLS_X     2
 #define MM_INFO_GRID_CELLS_Y     3
@@ -209,6 +210,7 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
 #define MM_INFO_DICT_OK          10
 #define MM_INFO_LAST_FORM        11
 #define MM_INFO_LAST_LDS_MODE    12
+#define MM_INFO_GRID_FACES       13
 int  mm_scene_info(const mm_ctx* ctx, int key, double* value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

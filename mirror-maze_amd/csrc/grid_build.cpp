@@ -121,7 +121,8 @@ uint32_t grid_records(const std::vector<uint32_t>& rc, uint32_t n_rects, std::ve
 // Cells of size ~s over the scene box widened by eps = C * 2^-14, their lists
 // and the image layout (recs and boxes are filled by the caller).
 bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint32_t>& recs, const double smin[3],
-                 const double smax[3], double C, double s, GridHost& g, std::string& why) {
+                 const double smax[3], double C, double s, bool wide, GridHost& g, std::string& why) {
+    g.wide = wide;
     g.n_glob = 0;
     const double eps = C * 0x1p-14;
     long total = 1;
@@ -163,6 +164,7 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
     }
     // counting sort of (cell, rect)
     std::vector<uint32_t> cnt(total + 1, 0);
+    std::vector<uint16_t> flat;
     for (int pass = 0; pass < 2; ++pass) {
         std::vector<uint32_t> cur(pass ? cnt : std::vector<uint32_t>());
         for (uint32_t k = 0; k < n_rects; ++k) {
@@ -172,12 +174,8 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
                 for (int y = sp.i0[1]; y <= sp.i1[1]; ++y)
                     for (int x = sp.i0[0]; x <= sp.i1[0]; ++x) {
                         const long c = ((long)z * g.n[1] + y) * g.n[0] + x;
-                        if (pass == 0) {
-                            cnt[c + 1]++;
-                        } else {
-                            uint16_t v = (uint16_t)k;
-                            std::memcpy(&g.image[g.off_list + 2 * (size_t)cur[c]++], &v, 2);
-                        }
+                        if (pass == 0) cnt[c + 1]++;
+                        else flat[cur[c]++] = (uint16_t)k;
                     }
         }
         if (pass == 0) {
@@ -185,19 +183,95 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
                 if (cnt[c + 1] >= 1024u) { why = "a cell lists 1024 or more rects"; return false; }
                 cnt[c + 1] += cnt[c];
             }
-            g.n_list = cnt[total];
-            if (g.n_list >= (1u << 22)) { why = "more than 2^22 list entries"; return false; }
-            g.off_list = align16(4u * (uint32_t)total);
-            g.off_recs = align16(g.off_list + 2u * g.n_list);
-            g.off_box = align16(g.off_recs + 32u * n_rects);
-            g.bytes = align16(g.off_box + 24u * n_rects);
-            g.image.assign(g.bytes, 0);
-            for (long c = 0; c < total; ++c) {
-                const uint32_t w = cnt[c] | ((cnt[c + 1] - cnt[c]) << 22);
-                std::memcpy(&g.image[4 * (size_t)c], &w, 4);
-            }
+            flat.assign(cnt[total], 0);
         }
     }
+    if (!wide) {  // plain 32-bit cell words: first entry | count << 22
+        if (cnt[total] >= (1u << 22)) { why = "more than 2^22 list entries"; return false; }
+        g.n_list = cnt[total];
+        g.off_list = align16(4u * (uint32_t)total);
+        g.off_recs = align16(g.off_list + 2u * g.n_list);
+        g.off_box = align16(g.off_recs + 32u * n_rects);
+        g.bytes = align16(g.off_box + 24u * n_rects);
+        g.image.assign(g.bytes, 0);
+        for (long c = 0; c < total; ++c) {
+            const uint32_t w = cnt[c] | ((cnt[c + 1] - cnt[c]) << 22);
+            std::memcpy(&g.image[4 * (size_t)c], &w, 4);
+        }
+        if (!flat.empty()) std::memcpy(&g.image[g.off_list], flat.data(), 2 * flat.size());
+        return true;
+    }
+    // Face ranges.  A query that steps into cell c through face f has tested
+    // every entry of the previous cell's list (by induction: the first cell's
+    // whole list, then each cell's range plus what the cell before it listed),
+    // so it need only test the entries of c that the neighbour across f does
+    // not list.  Each list is put in circular order around the cell (angle of
+    // the rect's box centre in the plane of the two axes with the most cells:
+    // in a maze the entries a neighbour shares are then adjacent) and stored
+    // with its first m - 1 entries repeated, so the entries to test form one
+    // range [start, start + len) for every face.  Face f = 2a + (0 when the
+    // query moved +a, 1 when it moved -a); the neighbour is on the -a / +a side.
+    int pl[3] = {0, 1, 2};
+    std::stable_sort(pl, pl + 3, [&](int x, int y) { return g.n[x] > g.n[y]; });
+    const int p0 = pl[0], p1 = pl[1];
+    std::vector<uint16_t> ext;
+    std::vector<uint64_t> words(total);
+    auto listed = [&](long c, uint16_t k) {
+        for (uint32_t q = cnt[c]; q < cnt[c + 1]; ++q)
+            if (flat[q] == k) return true;
+        return false;
+    };
+    for (long c = 0; c < total; ++c) {
+        const int ic[3] = {(int)(c % g.n[0]), (int)((c / g.n[0]) % g.n[1]), (int)(c / ((long)g.n[0] * g.n[1]))};
+        const uint32_t m = cnt[c + 1] - cnt[c];
+        const uint64_t base = ext.size();
+        if (base + 2 * (uint64_t)m >= (1u << 22)) { why = "more than 2^22 list entries"; return false; }
+        if (m > 7) {  // whole list for every face
+            for (uint32_t q = cnt[c]; q < cnt[c + 1]; ++q) ext.push_back(flat[q]);
+            words[c] = (1ull << 63) | ((uint64_t)m << 22) | base;
+            continue;
+        }
+        std::vector<std::pair<double, uint16_t>> e;
+        for (uint32_t q = cnt[c]; q < cnt[c + 1]; ++q) {
+            double lo[3], hi[3];
+            rect_box(rects[flat[q]], lo, hi);
+            const double c0 = g.mn[p0] + (ic[p0] + 0.5) * (double)g.cell[p0];
+            const double c1 = g.mn[p1] + (ic[p1] + 0.5) * (double)g.cell[p1];
+            e.push_back({std::atan2(0.5 * (lo[p1] + hi[p1]) - c1, 0.5 * (lo[p0] + hi[p0]) - c0), flat[q]});
+        }
+        std::stable_sort(e.begin(), e.end(), [](auto& x, auto& y) { return x.first < y.first; });
+        for (uint32_t i = 0; i < m; ++i) ext.push_back(e[i].second);
+        for (uint32_t i = 0; i + 1 < m; ++i) ext.push_back(e[i].second);
+        uint64_t w = base | ((uint64_t)m << 22);
+        for (int f = 0; f < 6; ++f) {
+            const int ax = f >> 1;
+            int nb[3] = {ic[0], ic[1], ic[2]};
+            nb[ax] += (f & 1) ? 1 : -1;
+            const bool inside = nb[ax] >= 0 && nb[ax] < g.n[ax];
+            const long cn = ((long)nb[2] * g.n[1] + nb[1]) * g.n[0] + nb[0];
+            bool keep[8];
+            uint32_t nk = 0;
+            for (uint32_t i = 0; i < m; ++i) nk += keep[i] = !(inside && listed(cn, e[i].second));
+            uint32_t bs = 0, bl = nk ? m : 0;
+            for (uint32_t st = 0; st < m && nk; ++st) {
+                if (!keep[st]) continue;
+                uint32_t len = 0;
+                for (uint32_t i = 0; i < m; ++i)
+                    if (keep[i]) len = std::max(len, (i + m - st) % m + 1);
+                if (len < bl) { bl = len; bs = st; }
+            }
+            w |= (uint64_t)(bs | (bl << 3)) << (25 + 6 * f);
+        }
+        words[c] = w;
+    }
+    g.n_list = (uint32_t)ext.size();
+    g.off_list = align16(8u * (uint32_t)total);
+    g.off_recs = align16(g.off_list + 2u * g.n_list);
+    g.off_box = align16(g.off_recs + 32u * n_rects);
+    g.bytes = align16(g.off_box + 24u * n_rects);
+    g.image.assign(g.bytes, 0);
+    std::memcpy(&g.image[0], words.data(), 8 * (size_t)total);
+    if (!ext.empty()) std::memcpy(&g.image[g.off_list], ext.data(), 2 * ext.size());
     return true;
 }
 
@@ -235,9 +309,11 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     std::nth_element(ext2.begin(), ext2.begin() + ext2.size() / 2, ext2.end());
     double s = ext2[ext2.size() / 2];
     for (int attempt = 0; attempt < 24; ++attempt, s *= 1.25) {
-        if (build_lists(rects, n_rects, recs, smin, smax, C, s, g, why) && 4.0 * g.n[0] * g.n[1] * g.n[2] +
-                                                                                   2.0 * g.n_list <= index_budget)
-            break;
+        // 64-bit cell words with face ranges where the whole image fits the
+        // budget, else plain 32-bit words at the same cell size, before
+        // coarser cells (the kernel variant for wide words stages all of it)
+        if (build_lists(rects, n_rects, recs, smin, smax, C, s, true, g, why) && g.bytes <= index_budget) break;
+        if (build_lists(rects, n_rects, recs, smin, smax, C, s, false, g, why) && g.off_recs <= index_budget) break;
         if (attempt == 23) { why = "no grid index fits the LDS budget"; return false; }
     }
     std::vector<uint32_t> grecs;

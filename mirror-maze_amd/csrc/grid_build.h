@@ -19,6 +19,7 @@ struct GridHost {
     uint32_t off_list = 0, off_recs = 0, off_box = 0, bytes = 0;
     uint32_t n_list = 0;
     uint32_t n_slow = 0;  // records the kernel tests with the general statement
+    bool wide = true;     // 64-bit cell words with face ranges (else 32-bit: first | count << 22)
     std::vector<uint8_t> image;
 };
 

@@ -19,7 +19,12 @@ constexpr int kStackMax = 50;     // shaders.metal:123
 // Closest-hit query methods of the wave-persistent kernel (MM_OPT_TRAVERSAL):
 // BVH loop forms (mm_trace.h) and the certified grid search (mm_grid.h).
 // kFormGridSlow (internal): the grid search on a scene with SLOW rect records.
-enum : int { kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7, kFormGrid = 11, kFormGridSlow = 12 };
+// kFormGridWide / kFormGridWideSlow (internal): the same on a grid with 64-bit
+// cell words (per-face list ranges; grid_build.cpp).
+enum : int {
+    kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7,
+    kFormGrid = 11, kFormGridSlow = 12, kFormGridWide = 13, kFormGridWideSlow = 14
+};
 
 // ---- HBM layouts ------------------------------------------------------------
 // Reference node (nodes_ref): 2 x float4 = the reference's 32-B bvh_node,
@@ -36,7 +41,7 @@ enum : int { kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7, kFormGrid = 11
 // (shaders.metal:52,60,61), computed once by k_prep_rects with the same ops.
 // Shade record: s0 = (color.rgb, is_mirror), s1 = emission (rgba).
 // Uniform grid of the certified search (mm_grid.h, built by grid_build.cpp).
-// The device image is one buffer: [cells: n_cells u32][list: u16, padded to
+// The device image is one buffer: [cells: n_cells u64][list: u16, padded to
 // 16 B][recs: 2 x uint4 per rect][box: 3 x float2 per rect]; the byte
 // offsets of the sections let a kernel stage it in LDS (all of it, records
 // first, or the cells + lists prefix).
@@ -46,7 +51,7 @@ struct DevGrid {
     int n[3];                  // cells per axis
     uint32_t n_glob;           // rects every query tests (cover > half the cells)
     uint32_t glob[4];
-    const uint32_t* cells;     // per cell: first list entry | count << 22
+    const void* cells;         // per cell: list base, count (and per-face ranges when wide; mm_grid.h)
     const uint16_t* list;      // rect indices
     const uint4* recs;         // per-rect grid records (grid_build.cpp; mm_grid.h: grid_rect)
     const float2* box;         // per rect: its reference leaf's box, (mn, mx) per axis

@@ -115,7 +115,7 @@ __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restric
 // Where the grid's arrays are read from (LDS or global memory).
 template <typename CellsT, typename ListT, typename RecsT, typename BoxT>
 struct GridView {
-    CellsT cells;  // per cell: first list entry | count << 22
+    CellsT cells;  // per cell: a 64-bit (wide) or 32-bit word (list range)
     ListT list;    // rect indices (u16)
     RecsT recs;    // 2 x uint4 per rect
     BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
@@ -151,7 +151,7 @@ __device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, floa
 // Search + certificate.  Returns true with (t, index) = the reference's answer
 // (t = kBig when nothing is hit), false when the caller must walk the BVH.
 // Requires sc.fast_ok && ray_fast_ok(r) && grid_ray_ok.
-template <bool kStats, bool kSlow, typename GV>
+template <bool kStats, bool kSlow, bool kWide, typename GV>
 __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const float4* __restrict__ geo,
                                             const Ray& r, float& t, uint32_t& index, Counters& c) {
     float best = kBig;
@@ -161,12 +161,31 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     int bx = grid_first(g, 0, r.o.x, r.y.x), by = grid_first(g, 1, r.o.y, r.y.y), bz = grid_first(g, 2, r.o.z, r.y.z);
     float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
           tz = grid_time(g, 2, bz, r.o.z, r.y.z);
-    auto cell_word = [&]() {
+    // Cell words (grid_build.cpp).  Wide (64-bit): bits 0-21 the list's first
+    // entry; bit 63 set: bits 22-31 the count, the whole list for every face;
+    // clear: bits 22-24 the count m <= 7, and per entry face f a 6-bit
+    // (start | len << 3) at bit 25 + 6f -- the range of the list the neighbour
+    // across f did not already hold.  Plain (32-bit): first | count << 22.
+    // face = 6: the whole list (the first cell).  (A run-time format flag
+    // cost 2 % on C3: the format is a template parameter.)
+    auto cell_range = [&](uint32_t face, uint32_t& j0, uint32_t& j1) {
         const int ix = r.y.x > 0.0f ? bx - 1 : bx, iy = r.y.y > 0.0f ? by - 1 : by, iz = r.y.z > 0.0f ? bz - 1 : bz;
-        return gv.cells[(iz * g.n[1] + iy) * g.n[0] + ix];
+        const uint32_t c = (uint32_t)((iz * g.n[1] + iy) * g.n[0] + ix);
+        if constexpr (kWide) {
+            const uint64_t cw = reinterpret_cast<const uint64_t*>(gv.cells)[c];
+            const bool whole = (cw >> 63) != 0;
+            const uint32_t m = (uint32_t)(cw >> 22) & (whole ? 0x3FFu : 7u);
+            const uint32_t fld = face < 6u ? (uint32_t)(cw >> (25u + 6u * face)) & 63u : (m << 3);
+            j0 = ((uint32_t)cw & 0x3FFFFFu) + (whole ? 0u : (fld & 7u));
+            j1 = j0 + (whole ? m : (fld >> 3));
+        } else {
+            const uint32_t cw = reinterpret_cast<const uint32_t*>(gv.cells)[c];
+            j0 = cw & 0x3FFFFFu;
+            j1 = j0 + (cw >> 22);
+        }
     };
-    uint32_t cw = cell_word();
-    uint32_t j = cw & 0x3FFFFFu, jend = j + (cw >> 22);
+    uint32_t j, jend;
+    cell_range(6u, j, jend);
     uint32_t cells = 1, tests = g.n_glob;
     // One iteration: test one rect of the current cell; when the cell's list
     // is done, step to the next cell (or stop) in the same iteration.
@@ -200,9 +219,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             tx = sx ? nt : tx;
             ty = sy ? nt : ty;
             tz = sz ? nt : tz;
-            cw = cell_word();
-            j = cw & 0x3FFFFFu;
-            jend = j + (cw >> 22);
+            cell_range((sx ? 0u : (sy ? 2u : 4u)) + ((sx ? r.y.x : (sy ? r.y.y : r.y.z)) > 0.0f ? 0u : 1u), j, jend);
             if (kStats) ++cells;
         }
     }

@@ -50,6 +50,7 @@ struct mm_ctx {
     DevGrid grid{};
     bool grid_ok = false;
     bool grid_slow = false;  // the grid has SLOW records (general rect test)
+    bool grid_wide = false;  // 64-bit cell words with per-face list ranges
     std::string grid_why;
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
@@ -143,7 +144,7 @@ void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_rects); (void)hipFree(c->d_nodes); (void)hipFree(c->d_nodes_ref); (void)hipFree(c->d_geo);
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
     (void)hipFree(c->d_grid);
-    c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false; c->grid_slow = false;
+    c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false; c->grid_slow = false; c->grid_wide = false;
     (void)hipFree(c->d_dict_tab); (void)hipFree(c->d_dict_words);
     c->d_dict_tab = nullptr; c->d_dict_words = nullptr; c->dict_ok = false;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
@@ -384,6 +385,7 @@ int mm_scene_info(const mm_ctx* c, int key, double* value) {
         case MM_INFO_DICT_OK: *value = c->dict_ok ? 1.0 : 0.0; return MM_OK;
         case MM_INFO_LAST_FORM: *value = c->last_form; return MM_OK;
         case MM_INFO_LAST_LDS_MODE: *value = c->last_mode; return MM_OK;
+        case MM_INFO_GRID_FACES: *value = c->grid_ok && c->grid_wide ? 1.0 : 0.0; return MM_OK;
         default: return MM_ERR_INVALID;
     }
 }
@@ -511,13 +513,14 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         }
         dg.n_glob = gh.n_glob;
         for (int i = 0; i < 4; ++i) dg.glob[i] = gh.glob[i];
-        dg.cells = reinterpret_cast<const uint32_t*>(c->d_grid);
+        dg.cells = c->d_grid;
         dg.list = reinterpret_cast<const uint16_t*>(c->d_grid + gh.off_list);
         dg.recs = reinterpret_cast<const uint4*>(c->d_grid + gh.off_recs);
         dg.box = reinterpret_cast<const float2*>(c->d_grid + gh.off_box);
         dg.image = reinterpret_cast<const uint4*>(c->d_grid);
         dg.off_list = gh.off_list; dg.off_recs = gh.off_recs; dg.off_box = gh.off_box; dg.bytes = gh.bytes;
         c->grid_slow = gh.n_slow > 0;
+        c->grid_wide = gh.wide;
     }
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     if (dict_ok) {
@@ -658,6 +661,11 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
         if (!c->grid_ok)
             return fail(c, MM_ERR_UNSUPPORTED, "grid search unavailable for this scene: " + c->grid_why);
         if (!c->lean_ok || c->grid_slow) form = kFormGridSlow;  // general rect tests for the SLOW records
+        if (c->grid_wide) {  // built only when the whole image fits the LDS budget (grid_build.cpp)
+            form += kFormGridWide - kFormGrid;
+            mode = c->opt_lds ? 11 : 13;
+            return MM_OK;
+        }
         if (c->opt_lds && c->grid.bytes <= budget) { mode = 11; return MM_OK; }
         if (c->opt_lds && c->grid.off_recs <= budget) { mode = 12; return MM_OK; }
         if (!auto_form || !c->opt_lds) { mode = 13; return MM_OK; }
@@ -789,7 +797,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
         if (persist) {
-            c->last_form = form == kFormGridSlow ? kFormGrid : form;
+            c->last_form = form >= kFormGrid ? kFormGrid : form;
             c->last_mode = mode;
             HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),

@@ -310,11 +310,11 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         staged();
         const char* base = reinterpret_cast<const char*>(lds);
         const char* index = base + 16u * nr16;
-        const auto gv = grid_view(reinterpret_cast<const uint32_t*>(index),
+        const auto gv = grid_view(reinterpret_cast<const char*>(index),
                                   reinterpret_cast<const uint16_t*>(index + sc.grid.off_list),
                                   reinterpret_cast<const uint4*>(lds),
                                   reinterpret_cast<const float2*>(base + (sc.grid.off_box - sc.grid.off_recs)));
-        return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
+        return body(GridQuery<kStats, kForm == kFormGridSlow || kForm == kFormGridWideSlow, kForm >= kFormGridWide, decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 12) {
         const uint32_t n16 = sc.grid.off_recs / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
@@ -322,13 +322,13 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         __syncthreads();
         staged();
         const char* base = reinterpret_cast<const char*>(lds);
-        const auto gv = grid_view(reinterpret_cast<const uint32_t*>(base),
+        const auto gv = grid_view(reinterpret_cast<const char*>(base),
                                   reinterpret_cast<const uint16_t*>(base + sc.grid.off_list), sc.grid.recs,
                                   sc.grid.box);
-        return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
+        return body(GridQuery<kStats, kForm == kFormGridSlow || kForm == kFormGridWideSlow, kForm >= kFormGridWide, decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 13) {
-        const auto gv = grid_view(sc.grid.cells, sc.grid.list, sc.grid.recs, sc.grid.box);
-        return body(GridQuery<kStats, kForm == kFormGridSlow, decltype(gv)>{sc, gv});
+        const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), sc.grid.list, sc.grid.recs, sc.grid.box);
+        return body(GridQuery<kStats, kForm == kFormGridSlow || kForm == kFormGridWideSlow, kForm >= kFormGridWide, decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 6) {
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
         __syncthreads();
@@ -473,6 +473,7 @@ static hipError_t launch_tail_t(const DevScene& sc, const TileJob& job, float4* 
 #define MM_DEFER_INSTANCES(X)                                                                                 \
     X(11, kFormGrid) X(12, kFormGrid) X(13, kFormGrid)                                                        \
     X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
+    X(11, kFormGridWide) X(13, kFormGridWide) X(11, kFormGridWideSlow) X(13, kFormGridWideSlow)               \
     X(3, kFormLean)
 #define MM_WP_INSTANCES(X)                                                                                    \
     MM_DEFER_INSTANCES(X) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                    \

@@ -39,7 +39,7 @@ MM_OPT_DEFER_MIN = 22
 MM_TRAV_AUTO, MM_TRAV_IFIF, MM_TRAV_LEAF_INTERIOR, MM_TRAV_LEAN, MM_TRAV_GRID = -1, 0, 5, 7, 11
 MM_INFO_GRID_OK, MM_INFO_GRID_CELLS_X, MM_INFO_GRID_CELLS_Y, MM_INFO_GRID_CELLS_Z = 1, 2, 3, 4
 MM_INFO_GRID_GLOBAL, MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_LEAN, MM_INFO_DEPTH = 5, 6, 7, 8, 9
-MM_INFO_DICT_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE = 10, 11, 12
+MM_INFO_DICT_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE, MM_INFO_GRID_FACES = 10, 11, 12, 13
 MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1

@@ -151,6 +151,71 @@ static void build_grid(double cell_target) {
     free(is_glob);
 }
 
+/* face ranges: each cell's list in circular order around the cell (angle of the
+   rect's box centre in the plane of the two axes with the most cells), stored
+   twice over (wrap), and per entered face the shortest circular range holding
+   every entry the neighbour across that face does not list */
+static uint32_t *fr_off, *fr_list;
+static uint8_t (*fr_s)[6], (*fr_l)[6];
+static int fr_on;
+static int listed_in(long c, uint32_t k) {
+    for (uint32_t q = cell_off[c]; q < cell_off[c + 1]; ++q) if (cell_list[q] == k) return 1;
+    return 0;
+}
+static void build_faces(void) {
+    fr_on = getenv("FACES") != NULL;
+    long total = (long)gn[0] * gn[1] * gn[2];
+    int ax0 = 0, ax1 = 2;  /* the plane: two axes with most cells */
+    { int o[3] = {0, 1, 2};
+      for (int i = 0; i < 3; ++i) for (int j = i + 1; j < 3; ++j) if (gn[o[j]] > gn[o[i]]) { int t = o[i]; o[i] = o[j]; o[j] = t; }
+      ax0 = o[0]; ax1 = o[1]; }
+    fr_off = malloc(8 * (total + 1)); fr_list = malloc(8 * (cell_off[total] + total + 1));
+    fr_s = malloc(6 * total); fr_l = malloc(6 * total);
+    uint32_t w = 0; uint64_t sum_full = 0, sum_face = 0, nf = 0;
+    for (long c = 0; c < total; ++c) {
+        int ic[3] = {(int)(c % gn[0]), (int)((c / gn[0]) % gn[1]), (int)(c / ((long)gn[0] * gn[1]))};
+        uint32_t m = cell_off[c + 1] - cell_off[c];
+        uint32_t e[64]; double ang[64];
+        if (m > 64) m = 64;
+        for (uint32_t i = 0; i < m; ++i) {
+            e[i] = cell_list[cell_off[c] + i];
+            double lo[3], hi[3]; rect_box(&S.rects[e[i]], lo, hi);
+            double cc0 = gmin[ax0] + (ic[ax0] + 0.5) * gcell[ax0], cc1 = gmin[ax1] + (ic[ax1] + 0.5) * gcell[ax1];
+            ang[i] = atan2(0.5 * (lo[ax1] + hi[ax1]) - cc1, 0.5 * (lo[ax0] + hi[ax0]) - cc0);
+        }
+        for (uint32_t i = 1; i < m; ++i) for (uint32_t j = i; j > 0 && ang[j] < ang[j - 1]; --j) {
+            double ta = ang[j]; ang[j] = ang[j - 1]; ang[j - 1] = ta; uint32_t te = e[j]; e[j] = e[j - 1]; e[j - 1] = te; }
+        fr_off[c] = w;
+        for (uint32_t i = 0; i < m; ++i) fr_list[w++] = e[i];
+        for (uint32_t i = 0; i + 1 < m; ++i) fr_list[w++] = e[i];
+        for (int f = 0; f < 6; ++f) {
+            int a = f >> 1, sgn = (f & 1) ? 1 : -1;  /* face f: neighbour at ic[a] + sgn */
+            int nb[3] = {ic[0], ic[1], ic[2]}; nb[a] += sgn;
+            int keep[64]; int nk = 0;
+            for (uint32_t i = 0; i < m; ++i) {
+                int in_nb = 0;
+                if (nb[a] >= 0 && nb[a] < gn[a]) in_nb = listed_in(((long)nb[2] * gn[1] + nb[1]) * gn[0] + nb[0], e[i]);
+                keep[i] = !in_nb; nk += keep[i];
+            }
+            uint32_t bs = 0, bl = m;
+            if (nk == 0) { bs = 0; bl = 0; }
+            else for (uint32_t st = 0; st < m; ++st) {
+                if (!keep[st]) continue;
+                uint32_t len = 0;
+                for (uint32_t i = 0; i < m; ++i) if (keep[i]) { uint32_t d = (i + m - st) % m + 1; if (d > len) len = d; }
+                if (len < bl) { bl = len; bs = st; }
+            }
+            fr_s[c][f] = (uint8_t)bs; fr_l[c][f] = (uint8_t)bl;
+            sum_full += m; sum_face += bl; nf++;
+        }
+    }
+    fr_off[total] = w;
+    { long h[20] = {0}; for (long c = 0; c < total; ++c) { uint32_t m = cell_off[c + 1] - cell_off[c]; h[m < 19 ? m : 19]++; }
+      fprintf(stderr, "list length hist:"); for (int i = 0; i < 20; ++i) if (h[i]) fprintf(stderr, " %d:%ld", i, h[i]); fprintf(stderr, "\n"); }
+    fprintf(stderr, "faces: list %u -> %u entries with wrap; mean full %.3f, mean face range %.3f\n", cell_off[total], w,
+            (double)sum_full / nf, (double)sum_face / nf);
+}
+
 /* ---------------------------------------------------------------- queries */
 /* reference rect test without the a < t clause: a, or BIG */
 static inline float rect_a(v3 ori, v3 dir, const mm_rect* r) {
@@ -168,7 +233,7 @@ static inline float rect_a(v3 ori, v3 dir, const mm_rect* r) {
 }
 
 typedef struct {
-    uint64_t queries, cells, tests, fallback_tie, fallback_verify, fallback_guard, mismatch, miss;
+    uint64_t big_face, dup_prev, dup_tests, queries, cells, tests, fallback_tie, fallback_verify, fallback_guard, mismatch, miss;
     uint64_t hist_cells[64];
 } gstats;
 
@@ -206,19 +271,34 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
     }
     int ncell = 0;
     q_n = 0;
+    uint32_t seen[256]; int n_seen = 0; long prev_c = -1; int face = -1;
     for (;;) {
         long c = ((long)ic[2] * gn[1] + ic[1]) * gn[0] + ic[0];
-        if (ncell < MAXC) q_len[ncell] = (int)(cell_off[c + 1] - cell_off[c]);
+        uint32_t j0 = cell_off[c], j1 = cell_off[c + 1];
+        const uint32_t* L = cell_list;
+        if (fr_on) {
+            L = fr_list; j0 = fr_off[c];
+            j1 = j0 + (face < 0 ? cell_off[c + 1] - cell_off[c] : fr_l[c][face]);
+            if (face >= 0 && fr_l[c][face] > 15) st->big_face++;
+            if (face >= 0 && getenv("NOY") && (face >> 1) == 1) j1 = j0 + cell_off[c + 1] - cell_off[c];
+            else if (face >= 0) { j0 += fr_s[c][face]; j1 += fr_s[c][face]; }
+        }
+        if (ncell < MAXC) q_len[ncell] = (int)(j1 - j0);
         ncell++;
         q_n = ncell < MAXC ? ncell : MAXC;
-        for (uint32_t j = cell_off[c]; j < cell_off[c + 1]; ++j) {
-            uint32_t k = cell_list[j];
+        for (uint32_t j = j0; j < j1; ++j) {
+            uint32_t k = L[j];
+            { int dup = 0; for (int q = 0; q < n_seen; ++q) if (seen[q] == k) dup = 1;
+              if (dup) st->dup_tests++; else if (n_seen < 256) seen[n_seen++] = k;
+              if (prev_c >= 0) for (uint32_t q = cell_off[prev_c]; q < cell_off[prev_c + 1]; ++q) if (cell_list[q] == k) { st->dup_prev++; break; } }
             consider(rect_a(o, d, &S.rects[k]), k, &best, &bk, &tie);
             st->tests++;
         }
         int a = tn[0] <= tn[1] ? (tn[0] <= tn[2] ? 0 : 2) : (tn[1] <= tn[2] ? 1 : 2);
+        prev_c = c;
         if (best < tn[a]) break;
         ic[a] += stp[a];
+        face = 2 * a + (stp[a] > 0 ? 0 : 1);  /* entered through the face toward the previous cell */
         if (ic[a] < 0 || ic[a] >= gn[a]) break;
         tn[a] = (gmin[a] + (float)(ic[a] + (stp[a] > 0)) * gcell[a] - oo[a]) * yy[a];
     }
@@ -316,6 +396,7 @@ int main(int argc, char** argv) {
     int W = atoi(argv[2]), H = atoi(argv[3]), spp = atoi(argv[4]), bl = atoi(argv[5]), ml = atoi(argv[6]);
     int rs = atoi(argv[7]);
     build_grid(argc > 8 ? atof(argv[8]) : 0.0);
+    build_faces();
     mm_uniform u;
     /* default camera (mm_uniform_default): centre (-5,0,-45), quat from (0.1,0,1), focal 1, viewport (2W/H, 2) */
     u.cam.center[0] = -5.0f; u.cam.center[1] = 0.0f; u.cam.center[2] = -45.0f; u.cam.focal = 1.0f;
@@ -406,7 +487,7 @@ int main(int argc, char** argv) {
           gnbmax += nbmax; gnbsum += nbsum; gnbw += nbw; for (int b = 0; b < 32; ++b) { gact[b] += act_hist[b]; git[b] += it_hist[b]; } }
 #pragma omp critical
         {
-            tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
+            tot.dup_tests += st.dup_tests; tot.dup_prev += st.dup_prev; tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
             tot.fallback_tie += st.fallback_tie; tot.fallback_verify += st.fallback_verify;
             tot.fallback_guard += st.fallback_guard; tot.mismatch += st.mismatch; tot.miss += st.miss;
             for (int i = 0; i < 64; ++i) tot.hist_cells[i] += st.hist_cells[i];
@@ -418,6 +499,7 @@ int main(int argc, char** argv) {
            (unsigned long long)tot.queries, tot.cells / q, tot.tests / q, 100 * tot.fallback_tie / q,
            100 * tot.fallback_verify / q, 100 * tot.fallback_guard / q, (unsigned long long)tot.miss,
            (unsigned long long)tot.mismatch);
+    printf("duplicate tests (rect already tested by this query) per query %.3f, of them listed in the previous cell %.3f\n", tot.dup_tests / q, tot.dup_prev / q);
     printf("wave model (VALU slots x64 per wave): nested %.4g  flat %.4g  ideal(lane work/64) %.4g  -> util nested %.3f flat %.3f\n",
            wnest, wflat, wlane / 64, wlane / 64 / wnest, wlane / 64 / wflat);
     printf("nested split: tests %.4g  cell steps %.4g  shading %.4g\n", wtest, wstep, wshade);

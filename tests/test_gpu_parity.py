@@ -378,6 +378,22 @@ def test_large_scene_bit_exact(gpu, opts):
     r.close()
 
 
+def test_grid_cell_formats(gpu):
+    """The grid build picks 64-bit cell words with per-face list ranges where
+    the index fits the LDS budget (C3's N=32 maze) and plain 32-bit words at
+    the same cell size otherwise (N=64), before coarser cells; both are
+    covered bit-exact by the whole-frame / window tests (test_gpu_frames.py)."""
+    from mirror_maze import MM_INFO_GRID_CELLS_X, MM_INFO_GRID_FACES, MM_INFO_GRID_OK, Renderer
+
+    for n, faces, cells_x in [(32, 1.0, 33), (64, 0.0, 65)]:
+        r = Renderer(0)
+        r.upload_scene(_scene(n))
+        assert r.scene_info(MM_INFO_GRID_OK) == 1.0
+        assert r.scene_info(MM_INFO_GRID_FACES) == faces, n
+        assert r.scene_info(MM_INFO_GRID_CELLS_X) == cells_x, n
+        r.close()
+
+
 def test_bench_prints_one_json_line(gpu):
     """bench.py's driver contract: exactly one JSON line on stdout with the
     metric, the roofline and the issue mode (short C2 run)."""
