@@ -92,11 +92,16 @@ def parse():
     p.add_argument("--contexts", type=int, default=0,
                    help="renderer contexts (one stream each) that consecutive frames alternate over; "
                         "0 = 1 on one GPU, 2 when the frame is split over ranks")
-    p.add_argument("--batch", type=int, default=8,
-                   help="frames per launch (mm_trace_tile_frames: the frames share one work queue, so the "
-                        "~0.4 ms launch tail is paid once per launch, not per frame); 1 = one frame per launch "
-                        "(then --contexts applies); 0 = time 1 context / 2 contexts / batches of 8 after warmup "
-                        "and keep the fastest")
+    p.add_argument("--batch", type=int, default=16,
+                   help="frames per launch at most (mm_trace_tile_frames: the frames share one work queue, so "
+                        "the launch's drain and its tail kernel are paid once per launch, not per frame); 1 = one "
+                        "frame per launch (then --contexts applies); 0 = time 1 context / 2 contexts / batches of "
+                        "8 after warmup and keep the fastest")
+    p.add_argument("--frame-format", default="rgba8", choices=["rgba8", "f32"],
+                   help="format of the frame each step delivers on rank 0: rgba8 = the reference's output "
+                        "texture format (RGBA8Unorm, src/main.rs:702-709; the texture-write conversion "
+                        "mm_quantize_rgba8 on each rank, then the gather moves 4 B/px), f32 = the float tile "
+                        "(16 B/px).  Accumulated runs (--accumulate) gather their f32 running sum.")
     p.add_argument("--accumulate", action="store_true",
                    help="temporal accumulation (C5): every frame adds into one running sum per rank "
                         "(MM_EXT_ACCUMULATE) and the frame is gathered once, after the last step")
@@ -242,7 +247,7 @@ def main():
     # renderer contexts on their own streams so frame k+1's blocks fill the
     # CUs frame k's tail leaves idle (two frames sharing the GPU run ~7 %
     # slower, profiles/r01_overlap_probe.txt; --contexts 0 times both).
-    n_ctx = (1 if args.accumulate or args.batch > 1 else (args.contexts if args.contexts > 0 else 2))
+    n_ctx = (1 if args.accumulate else args.contexts if args.contexts > 0 else 1 if args.batch > 1 else 2)
     rens = []
     for _ in range(n_ctx):
         r = Renderer(local)
@@ -261,24 +266,33 @@ def main():
     y0, y_stride, my_rows = row_shard(H, world, rank)
     if args.emulate_ranks > 1 and world == 1:
         y0, y_stride, my_rows = row_shard(H, args.emulate_ranks, 0)
-    frame_buf = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+    # the frame each step delivers: RGBA8 (the reference's texture format) or f32
+    rgba8 = args.frame_format == "rgba8" and not args.accumulate
+    fdt = torch.uint8 if rgba8 else torch.float32
+    frame_buf = torch.empty((H, W, 4), dtype=fdt, device=dev) if rank == 0 else None
     # one RCCL gather per frame, issued async on the frame's stream into
     # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
     # multi-frame launches need the wave-persistent kernel's fused resolve (64 % spp == 0)
     # (with the mirror-tail deferral -- the default -- samples are staged per frame, any spp)
     batchable = not args.accumulate
-    fb_max = (args.batch if args.batch > 0 else 8) if batchable else 1
+    fb_max = (min(args.batch, max(args.steps, args.warmup, 8)) if args.batch > 0 else 8) if batchable else 1
     # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,
     # so the next launch never waits on this batch's own gathers
-    gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf,
+    gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf, dtype=fdt,
                               slots=max(2, len(rens), 2 * fb_max if fb_max > 1 else 0),
                               assembly_stream=torch.cuda.Stream(dev))
                 if distributed else None)
-    tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in rens]
+    tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=fdt, device=dev) for _ in rens]
+    # float tiles the trace writes when the delivered frame is RGBA8 (one per context)
+    ftiles = [torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev) for _ in rens] if rgba8 else None
     last = [0]
     active = [len(rens)]  # contexts the frames alternate over
     batch = [1]           # frames per launch (mm_trace_tile_frames), single context
-    batch_buf = torch.zeros((fb_max, my_rows, W, 4), dtype=torch.float32, device=dev) if fb_max > 1 else None
+    # per context: the launch's float frames (and their RGBA8 conversions on one GPU)
+    batch_bufs = [torch.zeros((fb_max, my_rows, W, 4), dtype=torch.float32, device=dev) if fb_max > 1 else None
+                  for _ in rens]
+    batch_bufs8 = [torch.zeros((fb_max, my_rows, W, 4), dtype=torch.uint8, device=dev)
+                   if fb_max > 1 and rgba8 and not distributed else None for _ in rens]
     progress_t = [time.perf_counter()]
 
     def progress(msg):
@@ -300,36 +314,50 @@ def main():
                                               stats=stats)
                 return st
             tile = gatherer.tile() if gatherer else tiles1[slot]
+            ft = ftiles[slot] if rgba8 else tile
             _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
-                                          y_stride=y_stride, out=tile[:my_rows], stats=stats)
+                                          y_stride=y_stride, out=ft[:my_rows], stats=stats)
+            if rgba8:
+                rens[slot].quantize(ft[:my_rows], out=tile[:my_rows])
             if gatherer:
                 gatherer.put()
         last[0] = slot
         return st
 
-    def step_batch(k, frame, n, stats=False):
-        """n frames (frame, frame+1, ...) in one launch of context 0; each frame's tile then goes
-        to the gatherer (copied into its rotating tile) or stays in batch_buf."""
-        with torch.cuda.stream(streams[0]):
-            _, st = rens[0].trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), n, 0, y0, W, my_rows,
-                                              y_stride=y_stride, out=batch_buf[:n], stats=stats)
+    def step_batch(k, frame, n, slot=0, stats=False):
+        """n frames (frame, frame+1, ...) in one launch of context `slot`; each frame's tile then
+        goes to the gatherer (converted / copied into its rotating tile) or stays in the batch buffer."""
+        batch_buf, batch_buf8 = batch_bufs[slot], batch_bufs8[slot]
+        with torch.cuda.stream(streams[slot]):
+            _, st = rens[slot].trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), n, 0, y0, W, my_rows,
+                                                 y_stride=y_stride, out=batch_buf[:n], stats=stats)
             if gatherer:
                 for f in range(n):
-                    gatherer.tile()[:my_rows].copy_(batch_buf[f])
+                    if rgba8:
+                        rens[slot].quantize(batch_buf[f], out=gatherer.tile()[:my_rows])
+                    else:
+                        gatherer.tile()[:my_rows].copy_(batch_buf[f])
                     gatherer.put()
-        last[0] = 0
+            elif rgba8:  # every frame delivered in RGBA8
+                for f in range(n):
+                    rens[slot].quantize(batch_buf[f], out=batch_buf8[f])
+        last[0] = slot
         return st
 
     def run_frames(k0, frame0, count):
         """count frames starting at frame0 in the current issue mode"""
         if batch[0] > 1:
             i = n = 0
-            for n in launch_sizes(count, batch[0]):
-                step_batch(k0 + i, frame0 + i, n)
+            # launches alternate over the active contexts (their streams): with two, a launch's
+            # drain and tail kernel overlap the next launch
+            per = batch[0] if active[0] == 1 else min(batch[0], -(-count // active[0]))
+            for li, n in enumerate(launch_sizes(count, per)):
+                step_batch(k0 + i, frame0 + i, n, slot=li % active[0])
                 i += n
             if not gatherer and count > 0:  # the last frame, for frame_buf
-                with torch.cuda.stream(streams[0]):
-                    tiles1[0][:my_rows].copy_(batch_buf[n - 1])
+                sl = last[0]
+                with torch.cuda.stream(streams[sl]):
+                    tiles1[sl][:my_rows].copy_(batch_bufs8[sl][n - 1] if rgba8 else batch_bufs[sl][n - 1])
         else:
             for i in range(count):
                 step(k0 + i, frame0 + i)
@@ -354,15 +382,18 @@ def main():
             frame_buf.copy_(tiles1[last[0]])
 
     if fb_max > 1 and args.batch > 1:  # warm up the issue mode that is timed
-        batch[0] = fb_max
-        run_frames(0, 10_000, args.warmup)
+        active[0], batch[0] = len(rens), fb_max
+        # at least one launch of the timed launches' size: the context sizes its staging buffers
+        # and tail queue on the first launch that needs them (hipMalloc inside the timed region
+        # otherwise: 0.6 ms of a 6.4 ms 10-frame launch at C3 / rank 0 of 8)
+        run_frames(0, 10_000, max(args.warmup, min(args.steps, fb_max), len(rens)))
     else:
         for i in range(args.warmup):
             step(i, 10_000 + i)
     drain()
     calib = None
     if fb_max > 1 and args.batch > 1:
-        active[0], batch[0] = 1, fb_max
+        active[0], batch[0] = len(rens), fb_max
     elif (args.batch == 0 or args.contexts == 0) and not args.accumulate:
         # issue modes: one context, two alternating contexts, one context with batches of frames
         modes = [("1", 1, 1), ("2", 2, 1)] + ([(f"batch{fb_max}", 1, fb_max)] if args.batch == 0 and fb_max > 1
@@ -451,7 +482,7 @@ def main():
 
     if rank == 0:
         img = frame_buf.cpu().numpy()
-        assert np.isfinite(img).all(), "non-finite pixels"
+        assert np.isfinite(img).all() and img.any(), "non-finite or empty frame"
         value = rays_all / elapsed / 1e6
         # roofline of the dominant kernel (ray trace), rank 0's launches
         k_avg_s = (k_ms / 1e3) / max(k_launches, 1)
@@ -479,6 +510,7 @@ def main():
                        "parallelism": (f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU") +
                                       (f" (emulating rank 0 of {args.emulate_ranks})" if args.emulate_ranks > 1 else ""),
                        "frame_contexts": active[0],
+                       "frame_format": "rgba8" if rgba8 else "f32",
                        "frames_per_launch": (round(args.steps / max(k_launches, 1), 2) if batch[0] > 1 else 1),
                        "temporal_accumulation": bool(args.accumulate),
                        "options": args.opt or None,

@@ -821,13 +821,12 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             launches += 1;
             continue;
         }
-        const size_t fpaths = (size_t)job.w * job.h * job.e.spp, fpix = (size_t)job.w * job.h;
-        for (uint32_t f = 0; f < (defer ? n_frames : 1u); ++f) {  // frame f's samples -> its output slice
-            HIPC(c, launch_resolve(job, c->d_samples + f * fpaths,
-                                   reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w + f * fpix, c->stream));
-            launches += 1;
-        }
-        launches += 1;
+        // the frames' staged samples and output slices are contiguous (a multi-frame launch is one
+        // row batch), so one resolve over h x n_frames rows covers them all
+        TileJob rj = job;
+        if (defer) rj.h = job.h * n_frames;
+        HIPC(c, launch_resolve(rj, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
+        launches += 2;
     }
     if ((rc = end_timing(c, launches))) return rc;
     if (want_stats) return read_aux(c, stats);

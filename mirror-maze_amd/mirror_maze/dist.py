@@ -73,7 +73,7 @@ class FrameGatherer:
     the other stream's trace holds and delay that trace."""
 
     def __init__(self, shape, height: int, device, dst: int = 0, group=None, out=None, slots: int = 2,
-                 on_frame=None, assembly_stream=None):
+                 on_frame=None, assembly_stream=None, dtype=None):
         import torch
         import torch.distributed as dist
 
@@ -82,8 +82,9 @@ class FrameGatherer:
         self.rank = dist.get_rank(group)
         self.slots = slots
         self.on_frame = on_frame
-        self.tiles = [torch.zeros(shape, dtype=torch.float32, device=device) for _ in range(slots)]
-        self.bufs = ([[torch.empty(shape, dtype=torch.float32, device=device) for _ in range(self.world)]
+        dtype = torch.float32 if dtype is None else dtype
+        self.tiles = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(slots)]
+        self.bufs = ([[torch.empty(shape, dtype=dtype, device=device) for _ in range(self.world)]
                       for _ in range(slots)] if self.rank == dst else [None] * slots)
         self.k = 0
         self.pending = [None] * slots   # (frame index, Work) per slot

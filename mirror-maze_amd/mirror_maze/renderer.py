@@ -132,14 +132,17 @@ class Renderer:
         self._check(lib().mm_read_packets(self._ctx, out.ctypes.data, n_chunks))
         return out
 
-    def quantize(self, rgba):
-        """RGBA8 (uint8 CUDA tensor, same shape) of a float32 RGBA CUDA tensor,
-        with the texture-write conversion (mm_quantize_rgba8)."""
+    def quantize(self, rgba, out=None):
+        """RGBA8 (uint8 CUDA tensor, same shape; into `out` if given) of a float32
+        RGBA CUDA tensor, with the texture-write conversion (mm_quantize_rgba8)."""
         import torch
 
         if not (rgba.is_cuda and rgba.dtype == torch.float32 and rgba.is_contiguous() and rgba.shape[-1] == 4):
             raise ValueError("rgba must be a contiguous float32 CUDA tensor [..., 4]")
-        out = torch.empty(rgba.shape, dtype=torch.uint8, device=rgba.device)
+        if out is None:
+            out = torch.empty(rgba.shape, dtype=torch.uint8, device=rgba.device)
+        elif not (out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous() and out.shape == rgba.shape):
+            raise ValueError("out must be a contiguous uint8 CUDA tensor of rgba's shape")
         if not self._pinned_stream:
             self._check(lib().mm_set_stream(self._ctx, torch.cuda.current_stream(rgba.device).cuda_stream))
         self._check(lib().mm_quantize_rgba8(self._ctx, rgba.data_ptr(), out.data_ptr(), rgba.numel() // 4))

@@ -48,8 +48,10 @@ def _worker(rank, world, port, H, W, q):
     dist.destroy_process_group()
 
 
-def _worker_pipelined(rank, world, port, H, W, q):
-    """Three frames through FrameGatherer (async, double-buffered gathers)."""
+def _worker_pipelined(rank, world, port, H, W, q, fmt="f32"):
+    """Three frames through FrameGatherer (async, double-buffered gathers);
+    fmt "rgba8": each rank converts its tile to RGBA8 (the texture format,
+    mirror_maze.io.quantize) and the gather moves the uint8 tiles."""
     import sys
     from pathlib import Path
 
@@ -58,8 +60,11 @@ def _worker_pipelined(rank, world, port, H, W, q):
     sys.path.insert(0, str(repo / "mirror-maze_amd"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+
     from mirror_maze import Scene, default_uniform, make_ext
     from mirror_maze.dist import FrameGatherer, row_shard, rows_max
+    from mirror_maze.io import quantize
     from oracle.oracle import Oracle
 
     s = Scene.build(10, 0)
@@ -67,11 +72,16 @@ def _worker_pipelined(rank, world, port, H, W, q):
     u = default_uniform(W, H, 0)
     y0, stride, rows = row_shard(H, world, rank)
     frames = {}
-    g = FrameGatherer((rows_max(H, world), W, 4), H, "cpu",
+    g = FrameGatherer((rows_max(H, world), W, 4), H, "cpu", dtype=torch.uint8 if fmt == "rgba8" else None,
                       on_frame=lambda k, fr: frames.__setitem__(k, fr.numpy().copy()))
     for f in range(3):
         t = g.tile().numpy()
-        o.trace_tile(u, make_ext(2, 3, 15, frame=f), 0, y0, W, rows, y_stride=stride, out=t[:rows])
+        if fmt == "rgba8":
+            ft = np.zeros((rows, W, 4), dtype=np.float32)
+            o.trace_tile(u, make_ext(2, 3, 15, frame=f), 0, y0, W, rows, y_stride=stride, out=ft)
+            t[:rows] = quantize(ft)
+        else:
+            o.trace_tile(u, make_ext(2, 3, 15, frame=f), 0, y0, W, rows, y_stride=stride, out=t[:rows])
         g.put()
         if rank == 0:
             assert sorted(frames) == list(range(max(0, f - 1)))  # frame k completes when its slot is reused
@@ -83,15 +93,17 @@ def _worker_pipelined(rank, world, port, H, W, q):
     dist.destroy_process_group()
 
 
-def test_gloo_pipelined_gather_three_frames():
+@pytest.mark.parametrize("fmt", ["f32", "rgba8"])
+def test_gloo_pipelined_gather_three_frames(fmt):
     from mirror_maze import Scene, default_uniform, make_ext
+    from mirror_maze.io import quantize
     from oracle.oracle import Oracle
 
     world, H, W = 2, 9, 16
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, H, W, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, H, W, q, fmt)) for r in range(world)]
     for p in procs:
         p.start()
     frames = q.get(timeout=120)
@@ -101,7 +113,10 @@ def test_gloo_pipelined_gather_three_frames():
     o = Oracle.from_scene(Scene.build(10, 0))
     for f in range(3):
         ref, _ = o.trace_tile(default_uniform(W, H, 0), make_ext(2, 3, 15, frame=f), 0, 0, W, H)
-        assert np.array_equal(frames[f].view(np.uint32), ref.view(np.uint32)), f
+        if fmt == "rgba8":
+            assert frames[f].dtype == np.uint8 and np.array_equal(frames[f], quantize(ref)), f
+        else:
+            assert np.array_equal(frames[f].view(np.uint32), ref.view(np.uint32)), f
 
 
 @pytest.mark.parametrize("world,H", [(2, 12), (3, 10)])
