@@ -219,7 +219,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             tx = sx ? nt : tx;
             ty = sy ? nt : ty;
             tz = sz ? nt : tz;
-            cell_range((sx ? 0u : (sy ? 2u : 4u)) + ((sx ? r.y.x : (sy ? r.y.y : r.y.z)) > 0.0f ? 0u : 1u), j, jend);
+            cell_range((sx ? 0u : (sy ? 2u : 4u)) + (ya > 0.0f ? 0u : 1u), j, jend);  // (ya: by value, see above)
             if (kStats) ++cells;
         }
     }
