@@ -80,10 +80,21 @@ __device__ __forceinline__ bool bounce_loop(const DevScene& sc, const Q& query, 
             return true;
         float t = kBig;
         uint32_t k = 0;
+#ifdef MM_PHASE_CLOCKS
+        const uint64_t t0 = (uint64_t)wall_clock64();
+#endif
         const bool ok = query(p.ori, p.dir, t, k, stack, c);
+#ifdef MM_PHASE_CLOCKS
+        const uint64_t t1 = (uint64_t)wall_clock64();
+        c.q_cyc += t1 - t0;
+#endif
         if (kStats) c.rays++;
         if (!ok) { overflow = true; break; }
-        if (!shade_step(sc, p, t, k, mirror_limit)) break;
+        const bool more = shade_step(sc, p, t, k, mirror_limit);
+#ifdef MM_PHASE_CLOCKS
+        c.s_cyc += (uint64_t)wall_clock64() - t1;
+#endif
+        if (!more) break;
     }
     return false;
 }

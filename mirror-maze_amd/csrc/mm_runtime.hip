@@ -804,7 +804,10 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
                                              c->stream));
             if (defer) {
-                HIPC(c, launch_trace_tail(sc, job, c->d_samples, c->d_aux, reinterpret_cast<uint32_t*>(c->d_aux + 4),
+                TileJob tj = job;  // (the per-wave timeline records the main kernel)
+                tj.wave_ts = nullptr;
+                tj.wave_ts_cap = 0;
+                HIPC(c, launch_trace_tail(sc, tj, c->d_samples, c->d_aux, reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                           want_stats, mode, form, c->stream));
                 launches += 1;
             }

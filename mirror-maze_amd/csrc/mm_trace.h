@@ -30,6 +30,9 @@ namespace mm {
 
 struct Counters {
     uint32_t rays = 0, visits = 0, rtests = 0;
+#ifdef MM_PHASE_CLOCKS  // diagnostics build (scripts/phase_probe.py): wall_clock64 ticks (100 MHz) per phase
+    uint64_t q_cyc = 0, s_cyc = 0;
+#endif
 };
 
 struct Ray {

@@ -232,6 +232,22 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
         }
         if (job.fuse) resolve_in_wave(job, s, path, valid, job.out + (size_t)fr * job.w * job.h);
     }
+#ifdef MM_PHASE_CLOCKS
+    {  // the wave's time in queries / shading: the max over its lanes (some lane runs every iteration)
+        uint64_t qc = c.q_cyc, sc2 = c.s_cyc;
+        for (int o = 32; o > 0; o >>= 1) {
+            qc = max(qc, (uint64_t)__shfl_xor((unsigned long long)qc, o));
+            sc2 = max(sc2, (uint64_t)__shfl_xor((unsigned long long)sc2, o));
+        }
+        if (job.wave_ts && lane == 0) {
+            const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            if (wid < job.wave_ts_cap) {
+                job.wave_ts[4 * wid + 1] = qc;
+                job.wave_ts[4 * wid + 3] = sc2;
+            }
+        }
+    }
+#endif
     if (kStats) flush_stats(stats, c, paths);
     return chunks;
 }
@@ -295,7 +311,9 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
     auto staged = [&]() {  // diagnostics: time at which the block's LDS staging completed (wave timeline)
         if (job.wave_ts && (threadIdx.x & 63u) == 0) {
             const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+#ifndef MM_PHASE_CLOCKS
             if (wid < job.wave_ts_cap) job.wave_ts[4 * wid + 1] = (unsigned long long)wall_clock64();
+#endif
         }
     };
     if constexpr (kLds == 11) {
@@ -378,9 +396,14 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (wid < job.wave_ts_cap) {
+#ifdef MM_PHASE_CLOCKS  // (entry, query cycles, exit, shade cycles), s_memtime
+            job.wave_ts[4 * wid + 0] = t_entry;
+            job.wave_ts[4 * wid + 2] = (unsigned long long)wall_clock64();
+#else
             job.wave_ts[4 * wid + 0] = t_entry;
             job.wave_ts[4 * wid + 2] = (unsigned long long)wall_clock64();
             job.wave_ts[4 * wid + 3] = chunks;
+#endif
         }
     }
     if ((threadIdx.x & 63u) == 0) {
@@ -401,7 +424,11 @@ template <bool kStats, int kLds, int kForm, bool kDefer>
 __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {
+#ifdef MM_PHASE_CLOCKS
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
+#else
+    const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
+#endif
     const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
         return wavepersist_body<kStats, kDefer>(sc, q, job, samples, stats, err, work);
     });
