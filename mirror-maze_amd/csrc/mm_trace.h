@@ -473,6 +473,9 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         float len2 = dot3(rd, rd);
         // shaders.metal:316-318, length(r) > 1: RN(sqrt(x)) > 1 <=> x > 1 + 2^-23
         // for every binary32 x (exhaustive check: scripts/verify_sqrt_gt1.c)
+        // (a wave-pooled form of this loop -- the unluckiest lanes' trials spread
+        // over the others with jumps of the random() state -- was bit-exact and
+        // 12 % slower on C3, profiles/r02_ab_grid_salu.txt)
         while (len2 > 0x1.000002p0f) {
             rx = rand_pm1(p.seed); ry = rand_pm1(p.seed); rz = rand_pm1(p.seed);
             rd = F3{rx, ry, rz};

@@ -233,7 +233,7 @@ static inline float rect_a(v3 ori, v3 dir, const mm_rect* r) {
 }
 
 typedef struct {
-    uint64_t big_face, dup_prev, dup_tests, queries, cells, tests, fallback_tie, fallback_verify, fallback_guard, mismatch, miss;
+    uint64_t tail_q, tail_tests, tail_cells, big_face, dup_prev, dup_tests, queries, cells, tests, fallback_tie, fallback_verify, fallback_guard, mismatch, miss;
     uint64_t hist_cells[64];
 } gstats;
 
@@ -336,7 +336,9 @@ static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t
         (*rays)++;
         float gt; uint32_t gi;
         st->queries++;
+        const uint64_t t_before = st->tests, c_before = st->cells;
         int ok_q = grid_query(b.ori, b.dir, &gt, &gi, st);
+        if (n >= bl) { st->tail_q++; st->tail_tests += st->tests - t_before; st->tail_cells += st->cells - c_before; }
         if (n < MAXB) {
             w_n[w_lane][n] = q_n < 16 ? q_n : 16;
             for (int c = 0; c < w_n[w_lane][n]; ++c) w_len[w_lane][n][c] = q_len[c];
@@ -487,7 +489,7 @@ int main(int argc, char** argv) {
           gnbmax += nbmax; gnbsum += nbsum; gnbw += nbw; for (int b = 0; b < 32; ++b) { gact[b] += act_hist[b]; git[b] += it_hist[b]; } }
 #pragma omp critical
         {
-            tot.dup_tests += st.dup_tests; tot.dup_prev += st.dup_prev; tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
+            tot.dup_tests += st.dup_tests; tot.tail_q += st.tail_q; tot.tail_tests += st.tail_tests; tot.tail_cells += st.tail_cells; tot.dup_prev += st.dup_prev; tot.queries += st.queries; tot.cells += st.cells; tot.tests += st.tests;
             tot.fallback_tie += st.fallback_tie; tot.fallback_verify += st.fallback_verify;
             tot.fallback_guard += st.fallback_guard; tot.mismatch += st.mismatch; tot.miss += st.miss;
             for (int i = 0; i < 64; ++i) tot.hist_cells[i] += st.hist_cells[i];
@@ -499,6 +501,8 @@ int main(int argc, char** argv) {
            (unsigned long long)tot.queries, tot.cells / q, tot.tests / q, 100 * tot.fallback_tie / q,
            100 * tot.fallback_verify / q, 100 * tot.fallback_guard / q, (unsigned long long)tot.miss,
            (unsigned long long)tot.mismatch);
+    printf("queries past the bounce limit (mirror tails): %.3f%%, tests/query %.3f, cells/query %.3f\n",
+           100.0 * tot.tail_q / q, (double)tot.tail_tests / tot.tail_q, (double)tot.tail_cells / tot.tail_q);
     printf("duplicate tests (rect already tested by this query) per query %.3f, of them listed in the previous cell %.3f\n", tot.dup_tests / q, tot.dup_prev / q);
     printf("wave model (VALU slots x64 per wave): nested %.4g  flat %.4g  ideal(lane work/64) %.4g  -> util nested %.3f flat %.3f\n",
            wnest, wflat, wlane / 64, wlane / 64 / wnest, wlane / 64 / wflat);
