@@ -182,8 +182,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   default 16 (C3 5.92 -> 5.64 ms, profiles/r02_ab_defer.txt).  Built for the grid
                                   search and the lean BVH form with records in LDS; other forms ignore it */
 #define MM_OPT_DEFER_MIN  22  /* MM_OPT_DEFER applies to launches of at least this many paths (w*h*spp*frames;
-                                  default 2^21: on small launches the second kernel and the staged resolve cost
-                                  more than the tail saves, C1 0.135 vs 0.03 ms/frame); 0: always */
+                                  default 2^25: on smaller launches the tail kernel's fixed cost and the staged
+                                  resolve outweigh the tail saved -- C1 0.135 vs 0.03 ms/frame; 10 frames of
+                                  rank 0 of an 8-way C3 split, 20.7 M paths, 0.565 vs 0.550 ms/frame; 2-way,
+                                  83 M paths, 1.964 vs 2.037); 0: always */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Facts about the uploaded scene's search structures (double-valued):

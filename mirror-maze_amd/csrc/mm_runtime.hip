@@ -89,7 +89,7 @@ struct mm_ctx {
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
     int opt_defer = 16;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
-    uint32_t opt_defer_min = 1u << 21;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
+    uint32_t opt_defer_min = 1u << 25;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
