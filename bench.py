@@ -112,6 +112,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (approx)")
     p.add_argument("--src-hash", action="store_true", help="print the product source hash and exit")
+    p.add_argument("--save-frame", default="", help="rank 0 saves the last timed frame as it was delivered "
+                                                    "(.npy; tests/test_gpu_rccl.py checks it)")
     return p.parse_args()
 
 
@@ -482,6 +484,8 @@ def main():
 
     if rank == 0:
         img = frame_buf.cpu().numpy()
+        if args.save_frame:
+            np.save(args.save_frame, img)
         assert np.isfinite(img).all() and img.any(), "non-finite or empty frame"
         value = rays_all / elapsed / 1e6
         # roofline of the dominant kernel (ray trace), rank 0's launches

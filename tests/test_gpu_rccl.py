@@ -48,3 +48,40 @@ def test_rccl_gathered_frames_equal_trace_tile(gpu, tmp_path, config, frames):
         want, _ = r.trace_tile(u, make_ext(spp, bl, ml, frame=f), 0, 0, W, H)
         assert torch.equal(torch.from_numpy(got[f]).view(torch.int32), want.cpu().view(torch.int32)), f
     r.close()
+
+
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_bench_distributed_path_delivers_the_frame(gpu, tmp_path, config):
+    """bench.py exactly as the driver launches it for N GPUs (torchrun, the
+    "nccl" backend), at N = 1: batched launches, the RGBA8 conversion on the
+    rank, the RCCL gather and the de-interleave on rank 0.  The frame rank 0
+    holds after the timed steps must equal the texture-write conversion of
+    trace_tile's last frame, byte for byte (C2: one launch without tail
+    deferral; C3: three frames, 50 M paths, with it)."""
+    import json
+
+    import torch
+
+    from bench import CONFIGS
+    from mirror_maze import Renderer, Scene, default_uniform, make_ext
+
+    out = tmp_path / "frame.npy"
+    steps = 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"),
+           "--gpus", "1", "--config", config, "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline",
+           "--save-frame", str(out)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][-1])
+    assert line["n_gpus"] == 1 and line["config"]["frame_format"] == "rgba8"
+    assert "RCCL" in line["config"]["parallelism"]
+    got = np.load(out)
+    maze_n, W, H, spp, bl, ml, _ = CONFIGS[config]
+    r = Renderer(0)
+    r.upload_scene(Scene.build(maze_n, 0))
+    want, _ = r.trace_tile(default_uniform(W, H, 0), make_ext(spp, bl, ml, frame=steps - 1), 0, 0, W, H)
+    want8 = r.quantize(want).cpu().numpy()
+    assert got.dtype == np.uint8 and got.shape == (H, W, 4)
+    assert np.array_equal(got, want8)
+    r.close()
