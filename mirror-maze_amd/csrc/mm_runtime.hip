@@ -784,7 +784,11 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.y_stride = y_stride;
         job.view_w = W;
         job.fuse = fuse ? 1u : 0u;
+#ifdef MM_TAIL_TIMELINE
+        job.wave_ts = nullptr;
+#else
         job.wave_ts = c->d_wave_ts;
+#endif
         job.wave_ts_cap = c->wave_ts_cap;
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
@@ -805,8 +809,13 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                              c->stream));
             if (defer) {
                 TileJob tj = job;  // (the per-wave timeline records the main kernel)
+#ifdef MM_TAIL_TIMELINE  // diagnostics build: the tail kernel's waves instead
+                tj.wave_ts = c->d_wave_ts;
+                tj.wave_ts_cap = c->wave_ts_cap;
+#else
                 tj.wave_ts = nullptr;
                 tj.wave_ts_cap = 0;
+#endif
                 HIPC(c, launch_trace_tail(sc, tj, c->d_samples, c->d_aux, reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                           want_stats, mode, form, c->stream));
                 launches += 1;

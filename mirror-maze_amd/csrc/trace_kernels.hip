@@ -438,10 +438,11 @@ __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, Tile
 template <bool kStats, int kLds, int kForm>
 __global__ __launch_bounds__(1024, 8) void k_trace_tail(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                         unsigned long long* stats, uint32_t* err) {
+    const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
     const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
         return tail_body<kStats>(sc, q, job, samples, stats, err, nullptr);
     });
-    persistent_exit(job, chunks, 0ull, job.tail.count + 1, job.tail.count);
+    persistent_exit(job, chunks, t_entry, job.tail.count + 1, job.tail.count);
 }
 
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
