@@ -178,7 +178,7 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_DEFER      21  /* wave-persistent kernel: once at most this many lanes of a wave still trace
                                   (past bounce_limit only mirror-hit paths run on), those paths' states are queued
                                   and a second persistent kernel finishes them 64 to a wave; samples are then
-                                  staged per path and resolved by k_resolve (same order).  0 off, 1..63;
+                                  staged per path and resolved by k_resolve (same order).  0 off, 1..64;
                                   default 16 (C3 5.92 -> 5.64 ms, profiles/r02_ab_defer.txt).  Built for the grid
                                   search and the lean BVH form with records in LDS; other forms ignore it */
 #define MM_OPT_DEFER_MIN  22  /* MM_OPT_DEFER applies to launches of at least this many paths (w*h*spp*frames;

@@ -353,7 +353,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_reserve_cus = (uint32_t)value;
             return MM_OK;
         case MM_OPT_DEFER:
-            if (value < 0 || value > 63) return fail(c, MM_ERR_INVALID, "defer lanes must be 0..63");
+            if (value < 0 || value > 64) return fail(c, MM_ERR_INVALID, "defer lanes must be 0..64");
             c->opt_defer = value;
             return MM_OK;
         case MM_OPT_DEFER_MIN:

@@ -263,6 +263,9 @@ __device__ __forceinline__ uint32_t tail_body(const DevScene& sc, const Q& q, co
     Counters c;
     ScratchStack stack;
     uint32_t paths = 0, chunks = 0;
+#ifdef MM_TAIL_TIMELINE
+    uint32_t wave_iters = 0;
+#endif
     for (;;) {
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(tq.count + 1, 64u);
@@ -270,6 +273,9 @@ __device__ __forceinline__ uint32_t tail_body(const DevScene& sc, const Q& q, co
         if (base >= n) break;
         ++chunks;
         const uint32_t i = base + lane;
+#ifdef MM_TAIL_TIMELINE
+        int lane_bounces = 0;
+#endif
         if (i < n) {
             PathState p;
             p.ori = F3{tq.f(0)[i], tq.f(1)[i], tq.f(2)[i]};
@@ -281,15 +287,28 @@ __device__ __forceinline__ uint32_t tail_body(const DevScene& sc, const Q& q, co
             p.n = (int)(nm & 0xFFFFu);
             p.mh = (int)(nm >> 16);
             bool overflow = false;
+#ifdef MM_TAIL_TIMELINE
+            const int n0 = p.n;
+#endif
             bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
                                 1 << 30, 0u);
+#ifdef MM_TAIL_TIMELINE
+            lane_bounces = p.n - n0 + 1;
+#endif
             if (overflow) atomicOr(err, 1u);
             const F3 s = path_value(p);
             samples[tq.u(2)[i]] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
         }
+#ifdef MM_TAIL_TIMELINE  // the wave's bounce iterations for this chunk: its lanes' maximum
+        for (int o = 32; o > 0; o >>= 1) lane_bounces = max(lane_bounces, __shfl_xor(lane_bounces, o));
+        wave_iters += (uint32_t)lane_bounces;
+#endif
     }
     if (kStats) flush_stats(stats, c, paths);
+#ifdef MM_TAIL_TIMELINE
+    return wave_iters;
+#endif
     return chunks;
 }
 

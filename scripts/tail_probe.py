@@ -45,7 +45,7 @@ def main():
     print(f"# {desc}: tail kernel, {len(t)} waves, {a.frames} frames; times in us from the first wave's start")
     for q in (0, 10, 50, 90, 100):
         print(f"  p{q:3d}: start {np.percentile(start, q):8.1f}  staged {np.percentile(staged, q):8.1f}  "
-              f"end {np.percentile(end, q):8.1f}  chunks {np.percentile(chunks, q):6.1f}")
+              f"end {np.percentile(end, q):8.1f}  chunks|iters {np.percentile(chunks, q):6.1f}")
     print(f"  sum of chunks {chunks.sum():.0f}; busy share (sum of wave lives / (waves x span)) "
           f"{(end - start).sum() / (len(t) * end.max()):.3f}")
     r.close()
