@@ -33,6 +33,14 @@
 // exact.  scripts/grid_sim.c replays every query of a C3 frame (137 M) on
 // the CPU against the reference walk: 0 differences.
 //
+// Face ranges (64-bit cell words): a cell entered through face f tests only
+// the entries the neighbour across f -- the cell visited just before -- does
+// not list.  Every entry of every visited cell's list is still tested: by
+// induction, the first cell tests its whole list, and an entry of cell i that
+// is skipped is on cell i-1's list, all of which was tested by then.  Testing a
+// rect twice never changes (best, bk, tie) (same a, same k), so skipping the
+// repeat changes nothing.
+//
 // A tie, a failed leaf-box check or a ray outside the Markstein guards /
 // the grid runs the reference walk (the BVH traversal) instead.
 #pragma once
