@@ -150,3 +150,39 @@ def test_c5_temporal_accumulation_three_frames(gpu):
         assert np.all(got[..., 3] == 3.0)
         assert _diff(got, ref) == 0, (x0, y0)
     r.close()
+
+
+@pytest.mark.parametrize("cell,direction", [((3, 4), (1.0, 0.05, 0.2)), ((16, 16), (-0.3, -0.1, 1.0)),
+                                            ((30, 2), (0.7, 0.3, -0.6)), ((0, 31), (0.0, -0.2, -1.0))],
+                         ids=["corridor", "centre", "corner-up", "edge-down"])
+def test_cameras_inside_the_maze(gpu, cell, direction):
+    """C3's scene and limits with the camera inside the maze (cell centres,
+    assorted view directions, quaternion by calculate_quaternion,
+    src/maths.rs:139-156): whole 320x180 frames at 8 spp vs the oracle.  The
+    bench camera looks along the outer wall; these rays start in corridors,
+    exercise every face range of the grid and the mirrors at close range."""
+    from mirror_maze import MM_PIPE_AUTO, Renderer, calculate_quaternion, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(32)
+    base = -10.0 * (32 / 2)
+    u = default_uniform(320, 180, 0)
+    u.cam.center[0] = base + 10.0 * cell[0] + 5.0
+    u.cam.center[1] = 0.0
+    u.cam.center[2] = base + 10.0 * cell[1] + 5.0
+    q = calculate_quaternion(np.asarray(direction, dtype=np.float32))
+    for i in range(4):
+        u.cam.quat[i] = float(q[i])
+    e = make_ext(8, 8, 8, frame=3)
+    ref, n = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 320, 180)
+    assert n > 4 * 320 * 180 * 8 and ref[..., :3].mean() > 0.01  # the paths bounce inside the maze
+    for opts in ({}, {22: 0}):  # fused resolve; tail deferral with staged samples
+        r = Renderer(0)
+        r.set_pipeline(MM_PIPE_AUTO)
+        for k, v in opts.items():
+            r.set_option(k, v)
+        r.upload_scene(s)
+        got, st = r.trace_tile(u, e, 0, 0, 320, 180, stats=True)
+        assert _diff(got.cpu().numpy(), ref) == 0, opts
+        assert st.rays == n
+        r.close()
