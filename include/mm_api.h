@@ -176,16 +176,16 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   1 when the plain nodes do not fit and no explicit split size is set (default),
                                   2 always when it fits (tests), 0 off */
 #define MM_OPT_DEFER      21  /* wave-persistent kernel: once at most this many lanes of a wave still trace
-                                  (past bounce_limit only mirror-hit paths run on), those paths' states are queued
-                                  and a second persistent kernel finishes them 64 to a wave; samples are then
-                                  staged per path and resolved by k_resolve (same order).  0 off, 1..64;
-                                  default 16 (C3 5.92 -> 5.64 ms, profiles/r02_ab_defer.txt).  Built for the grid
-                                  search and the lean BVH form with records in LDS; other forms ignore it */
+                                  (past bounce_limit only mirror-hit paths run on), those paths' states go to
+                                  their block's tail ring (512 entries) and the block's waves take 64 of them at
+                                  a time as a chunk of their own; samples are then staged per path and resolved
+                                  by k_resolve (same order).  0 off, 1..64; default 32 (C3 3.27 ms vs 3.71 with
+                                  0, profiles/r02_ab_ring.txt).  Built for the grid search and the lean BVH form
+                                  with records in LDS; other forms ignore it */
 #define MM_OPT_DEFER_MIN  22  /* MM_OPT_DEFER applies to launches of at least this many paths (w*h*spp*frames;
-                                  default 2^25: on smaller launches the tail kernel's fixed cost and the staged
-                                  resolve outweigh the tail saved -- C1 0.135 vs 0.03 ms/frame; 10 frames of
-                                  rank 0 of an 8-way C3 split, 20.7 M paths, 0.565 vs 0.550 ms/frame; 2-way,
-                                  83 M paths, 1.964 vs 2.037); 0: always */
+                                  default 2^24: below it the staged resolve outweighs the tail saved -- C1
+                                  0.039 vs 0.033 ms/frame, C2 x 5 frames 0.49 vs 0.42; 10 frames of rank 0 of an
+                                  8-way C3 split, 20.7 M paths, 0.50 vs 0.51); 0: always */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Facts about the uploaded scene's search structures (double-valued):

@@ -133,9 +133,15 @@ __device__ __forceinline__ GridView<C, L, R, B> grid_view(C c, L l, R r, B b) {
     return GridView<C, L, R, B>{c, l, r, b};
 }
 
+// (&=, not &&: see ray_fast_ok)
 __device__ __forceinline__ bool grid_ray_ok(const DevGrid& g, const Ray& r) {
-    return r.o.x >= g.mn[0] && r.o.x <= g.mx[0] && r.o.y >= g.mn[1] && r.o.y <= g.mx[1] && r.o.z >= g.mn[2] &&
-           r.o.z <= g.mx[2];
+    bool ok = r.o.x >= g.mn[0];
+    ok &= r.o.x <= g.mx[0];
+    ok &= r.o.y >= g.mn[1];
+    ok &= r.o.y <= g.mx[1];
+    ok &= r.o.z >= g.mn[2];
+    ok &= r.o.z <= g.mx[2];
+    return ok;
 }
 
 __device__ __forceinline__ int grid_cell(const DevGrid& g, float o, int a) {

@@ -17,19 +17,17 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
                                uint32_t grid_w, uint32_t grid_h, float4* fb, uint32_t* fb8,
                                unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
 
-// Queue of deferred path states, SoA (one array per field, `cap` entries):
-// f[0..11] = ori, dir, T, L (x, y, z each); u[0] seed, u[1] n | mh << 16,
-// u[2] sample slot.  count[0] = slots reserved (the trace kernel's waves
-// reserve with one atomic each; a wave whose reservation would pass `cap`
-// does not defer), count[1] = next entry for the tail kernel, count[2] =
-// tail waves done; the tail kernel's last wave re-zeroes all three.
+// Deferred path states (mirror-tail deferral): one 64-byte record per entry
+// (rec[4*i .. 4*i+3] = ori.xyz dir.x | dir.yz T.xy | T.z L.xyz | seed,
+// n | mh << 16, sample slot, 0 -- one base pointer; 15 SoA field arrays would
+// hold 15 addresses in SGPRs across the bounce loop), `cap` records; resident
+// block b owns the kTailRing records from b * kTailRing (its tail ring, at most
+// 2 blocks per CU).
+constexpr uint32_t kTailRing = 512;
+
 struct TailQueue {
-    float* base = nullptr;     // field i at base + i * stride
-    uint32_t stride = 0;
+    uint4* rec = nullptr;
     uint32_t cap = 0;
-    uint32_t* count = nullptr;
-    __host__ __device__ float* f(int i) const { return base + (size_t)i * stride; }
-    __host__ __device__ uint32_t* u(int i) const { return reinterpret_cast<uint32_t*>(base + (size_t)(12 + i) * stride); }
 };
 
 struct TileJob {
@@ -56,9 +54,10 @@ struct TileJob {
     // Mirror-tail deferral (MM_OPT_DEFER; wave-persistent kernel, samples
     // staged per path, no fused resolve): a wave whose paths are at bounce
     // >= defer_from with at most defer_lanes lanes still running queues those
-    // paths' state (ballot + prefix compaction, one atomic per wave) and
-    // moves on; k_trace_tail finishes the queue densely.  Sample slot of a
-    // path: fr * (w*h*spp) + path.  defer_from >= 2^30: off.
+    // paths' state in its block's tail ring (ballot + prefix compaction, one
+    // LDS atomic per wave) and moves on; the block's waves take 64 queued tails
+    // at a time as a chunk.  Sample slot of a path: fr * (w*h*spp) + path.
+    // defer_from >= 2^30: off.
     uint32_t defer_from = 1u << 30, defer_lanes = 0;
     TailQueue tail;
 };
@@ -86,12 +85,6 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
 // Whether the tail-deferral variant exists for this (LDS mode, form).
 bool wavepersist_defer_built(int lds_mode, int form);
-// The deferred mirror tails of the last wave-persistent launch (same scene data
-// placement and query method): persistent blocks drain job.tail, writing each
-// finished path's sample value to samples[slot].
-hipError_t launch_trace_tail(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
-                             uint32_t* err, bool count_stats, int lds_mode, int form, hipStream_t s);
-
 // Display stage (display.hip).
 hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H, hipStream_t s);
 hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,

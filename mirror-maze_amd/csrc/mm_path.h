@@ -38,46 +38,28 @@ struct GridQuery {
     __device__ __forceinline__ bool operator()(F3 o, F3 d, float& t, uint32_t& k, ScratchStack& st,
                                                Counters& c) const {
         const Ray r = make_ray(o, d);
-        if (sc.fast_ok && ray_fast_ok(r) && grid_ray_ok(sc.grid, r) &&
-            grid_search<kStats, kSlow, kWide>(sc.grid, gv, sc.geo, r, t, k, c))
-            return true;
+        bool guards = sc.fast_ok != 0;  // one branch for the three guards
+        guards &= ray_fast_ok(r);
+        guards &= grid_ray_ok(sc.grid, r);
+        if (guards && grid_search<kStats, kSlow, kWide>(sc.grid, gv, sc.geo, r, t, k, c)) return true;
         t = kBig;  // (an out-of-line walk costs 73 VGPR spills of call ABI)
         return closest_hit_bvh<kStats, kSlow ? kFormLeafInterior : kFormLean>(sc, view(sc.nodes, sc.recs), r, t, k,
                                                                               st, c);
     }
 };
 
-// Deferral of a wave's last live lanes: reserve queue slots for the lanes
-// executing this (one atomic per wave, slots by prefix popcount).  A lane
-// whose slot is past the queue's capacity does not defer (it goes on), so the
-// entries below the capacity are exactly the written ones.
-__device__ __forceinline__ bool defer_reserve(uint32_t* count, uint32_t cap, uint32_t& slot) {
-    const uint64_t m = __ballot(1);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    const uint32_t cnt = (uint32_t)__popcll(m);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, cnt);
-    base = __shfl(base, (int)leader);
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    slot = base + (uint32_t)__popcll(m & lt);
-    return slot < cap;
-}
-
 // The bounce loop of shaders.metal:306-340 from state p (p.n bounces done).
 // Deferral: at the top of a bounce n >= defer_from, if at most defer_lanes
-// lanes of the wave are still in the loop and queue slots are left, those
-// lanes stop and return true with p holding the state the next bounce starts
-// from and `slot` their queue entry.  defer_from >= 2^30: never.
-template <bool kStats, typename Q>
-__device__ __forceinline__ bool bounce_loop(const DevScene& sc, const Q& query, PathState& p, int bounce_limit,
-                                            int mirror_limit, ScratchStack& stack, Counters& c, bool& overflow,
-                                            int defer_from, uint32_t defer_lanes, uint32_t* qcount = nullptr,
-                                            uint32_t qcap = 0, uint32_t* slot = nullptr) {
+// lanes of the wave are still in the loop and reserve() (called by those
+// lanes together) grants them queue entries, those lanes stop and return true
+// with p holding the state the next bounce starts from.  defer_from >= 2^30:
+// never.
+template <bool kStats, typename Q, typename Reserve>
+__device__ __forceinline__ bool bounce_loop_r(const DevScene& sc, const Q& query, PathState& p, int bounce_limit,
+                                              int mirror_limit, ScratchStack& stack, Counters& c, bool& overflow,
+                                              int defer_from, uint32_t defer_lanes, Reserve&& reserve) {
     for (; p.n < bounce_limit + p.mh; ++p.n) {
-        if (p.n >= defer_from && (uint32_t)__popcll(__ballot(1)) <= defer_lanes &&
-            defer_reserve(qcount, qcap, *slot))
-            return true;
+        if (p.n >= defer_from && (uint32_t)__popcll(__ballot(1)) <= defer_lanes && reserve()) return true;
         float t = kBig;
         uint32_t k = 0;
 #ifdef MM_PHASE_CLOCKS
@@ -99,6 +81,14 @@ __device__ __forceinline__ bool bounce_loop(const DevScene& sc, const Q& query, 
     return false;
 }
 
+// The bounce loop without deferral.
+template <bool kStats, typename Q>
+__device__ __forceinline__ void bounce_loop(const DevScene& sc, const Q& query, PathState& p, int bounce_limit,
+                                            int mirror_limit, ScratchStack& stack, Counters& c, bool& overflow) {
+    bounce_loop_r<kStats>(sc, query, p, bounce_limit, mirror_limit, stack, c, overflow, 1 << 30, 0u,
+                          []() { return false; });
+}
+
 // Whole path (shaders.metal:302-344): returns sqrt(max(L, 0)).
 template <bool kStats, typename Q>
 __device__ __forceinline__ F3 trace_path(const DevScene& sc, const Q& query, F3 ori, F3 dir, uint32_t seed,
@@ -110,7 +100,7 @@ __device__ __forceinline__ F3 trace_path(const DevScene& sc, const Q& query, F3 
     p.L = F3{0.0f, 0.0f, 0.0f};
     p.n = 0;
     p.mh = 0;
-    bounce_loop<kStats>(sc, query, p, bounce_limit, mirror_limit, stack, c, overflow, 1 << 30, 0u);
+    bounce_loop<kStats>(sc, query, p, bounce_limit, mirror_limit, stack, c, overflow);
     return F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))};
 }
 

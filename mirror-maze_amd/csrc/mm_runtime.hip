@@ -69,7 +69,7 @@ struct mm_ctx {
     // per-sample staging (throughput mode)
     float4* d_samples = nullptr;
     size_t samples_cap = 0;
-    // mirror-tail queue (MM_OPT_DEFER)
+    // mirror-tail rings' records (MM_OPT_DEFER)
     void* d_tail = nullptr;
     uint32_t tail_cap = 0;
     // aux: stats[4] (u64) + error flag (u32)
@@ -88,8 +88,8 @@ struct mm_ctx {
     bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
-    int opt_defer = 16;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
-    uint32_t opt_defer_min = 1u << 25;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
+    int opt_defer = 32;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
+    uint32_t opt_defer_min = 1u << 24;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
@@ -191,23 +191,20 @@ bool extent_ok(float x) {
     return a == 0.0f || (a >= 0x1p-10f && a <= 0x1p60f);
 }
 
-// The mirror-tail queue (mm_launch.h TailQueue): 15 SoA arrays of `cap`
-// entries + 3 counters, one allocation; the counters start at zero and the
-// tail kernel's last wave re-zeroes them.
-int tail_queue(mm_ctx* c, uint32_t cap, TailQueue& q) {
-    const size_t n4 = ((size_t)cap + 63) & ~(size_t)63;
+// The tail rings' records (mm_launch.h TailQueue): kTailRing per resident
+// block, at most 2 blocks per CU.
+int tail_queue(mm_ctx* c, TailQueue& q) {
+    int cus = 0;
+    HIPC(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    const uint32_t cap = 2u * (uint32_t)cus * kTailRing;
     if (c->tail_cap < cap || !c->d_tail) {
         (void)hipFree(c->d_tail);
         c->d_tail = nullptr;
         c->tail_cap = 0;
-        HIPC(c, hipMalloc(&c->d_tail, (15 * n4 + 64) * 4));
-        HIPC(c, hipMemsetAsync(reinterpret_cast<uint32_t*>(c->d_tail) + 15 * n4, 0, 64 * 4, c->stream));
+        HIPC(c, hipMalloc(&c->d_tail, (size_t)cap * 64));
         c->tail_cap = cap;
     }
-    const size_t m4 = ((size_t)c->tail_cap + 63) & ~(size_t)63;
-    q.base = reinterpret_cast<float*>(c->d_tail);
-    q.stride = (uint32_t)m4;
-    q.count = reinterpret_cast<uint32_t*>(c->d_tail) + 15 * m4;
+    q.rec = reinterpret_cast<uint4*>(c->d_tail);
     q.cap = c->tail_cap;
     return MM_OK;
 }
@@ -242,6 +239,7 @@ int read_aux(mm_ctx* c, mm_stats* st) {
     if (st) { st->rays = h[0]; st->node_visits = h[1]; st->rect_tests = h[2]; st->paths = h[3]; }
     if ((uint32_t)h[4] != 0) {
         HIPC(c, hipMemsetAsync(c->d_aux + 4, 0, sizeof(unsigned long long), c->stream));
+        if (h[4] & 2u) return fail(c, MM_ERR_HIP, "tail ring wait timed out (kernel protocol error)");
         return fail(c, MM_ERR_STACK, "traversal stack overflow (depth > 50)");
     }
     return MM_OK;
@@ -725,7 +723,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     // (32 Mi in the wavefront pipeline).  With the fused resolve there is no
     // staging buffer: one launch covers up to 2^31 paths (a whole C5 frame).
     const uint64_t row_paths = (uint64_t)w * e->spp;
-    // MM_PIPE_WAVEFRONT: the wave-persistent kernel with the compacted mirror-tail queue always on
+    // MM_PIPE_WAVEFRONT: the wave-persistent kernel with mirror-tail deferral (compaction) always on
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
     const bool persist = c->pipe != MM_PIPE_REFERENCE && (wave || c->opt_persist == 2);
     int form = 0, mode = 0;
@@ -734,7 +732,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         int rc0 = choose_wavepersist(c, sc, form, mode);
         if (rc0) return rc0;
     }
-    // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run by k_trace_tail; built for
+    // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run from block-local rings; built for
     // the grid search and the lean BVH form with records in LDS (other forms run without it)
     const bool defer = persist && (c->opt_defer > 0 || wave) && wavepersist_defer_built(mode, form) &&
                        (wave || (uint64_t)w * h * e->spp * n_frames >= c->opt_defer_min);
@@ -761,11 +759,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                    (size_t)(row_paths * rows_per_batch) * (defer ? n_frames : 1));
     if (rc) return rc;
     TailQueue tq;
-    if (defer) {  // queue capacity: a quarter of the paths (a wave past it does not defer)
-        const uint32_t cap = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull >> 2,
-                                                          row_paths * rows_per_batch * n_frames / 4 + 65536);
-        if ((rc = tail_queue(c, cap, tq))) return rc;
-    }
+    if (defer && (rc = tail_queue(c, tq))) return rc;
     // aux: [0..3] stats (zeroed only when counted), [4] sticky error flag
     // (cleared by read_aux), [5] lane-refill counter (zeroed by its launcher),
     // [6] wave-persistent counter pair (self-cleaning).  No fill kernel on the
@@ -784,18 +778,14 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.y_stride = y_stride;
         job.view_w = W;
         job.fuse = fuse ? 1u : 0u;
-#ifdef MM_TAIL_TIMELINE
-        job.wave_ts = nullptr;
-#else
         job.wave_ts = c->d_wave_ts;
-#endif
         job.wave_ts_cap = c->wave_ts_cap;
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
         job.reserve_cus = c->opt_reserve_cus;
         if (defer) {
             job.defer_from = 1;
-            job.defer_lanes = c->opt_defer > 0 ? (uint32_t)c->opt_defer : 16u;
+            job.defer_lanes = c->opt_defer > 0 ? (uint32_t)c->opt_defer : 32u;
             job.tail = tq;
         }
         if ((rc = prof_mark(c))) return rc;
@@ -807,19 +797,6 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                              reinterpret_cast<uint32_t*>(c->d_aux + 4),
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
                                              c->stream));
-            if (defer) {
-                TileJob tj = job;  // (the per-wave timeline records the main kernel)
-#ifdef MM_TAIL_TIMELINE  // diagnostics build: the tail kernel's waves instead
-                tj.wave_ts = c->d_wave_ts;
-                tj.wave_ts_cap = c->wave_ts_cap;
-#else
-                tj.wave_ts = nullptr;
-                tj.wave_ts_cap = 0;
-#endif
-                HIPC(c, launch_trace_tail(sc, tj, c->d_samples, c->d_aux, reinterpret_cast<uint32_t*>(c->d_aux + 4),
-                                          want_stats, mode, form, c->stream));
-                launches += 1;
-            }
         } else {
             MegaOpts mo;
             mo.reference = c->pipe == MM_PIPE_REFERENCE;

@@ -51,14 +51,27 @@ __device__ __forceinline__ Ray make_ray(F3 o, F3 d) {
 // Exponent guards for the Markstein quotient (see header comment).
 __device__ __forceinline__ bool dir_ok(float x) {
     const float a = fabsf(x);
-    return a >= 0x1p-40f && a <= 0x1p40f;
+    bool ok = a >= 0x1p-40f;
+    ok &= a <= 0x1p40f;
+    return ok;
 }
 __device__ __forceinline__ bool org_ok(float x) {
     const float a = fabsf(x);
-    return a == 0.0f || (a >= 0x1p-30f && a <= 0x1p60f);
+    bool in = a >= 0x1p-30f;
+    in &= a <= 0x1p60f;
+    in |= a == 0.0f;
+    return in;
 }
 __device__ __forceinline__ bool ray_fast_ok(const Ray& r) {
-    return dir_ok(r.d.x) && dir_ok(r.d.y) && dir_ok(r.d.z) && org_ok(r.o.x) && org_ok(r.o.y) && org_ok(r.o.z);
+    // (&=, not &&: a short-circuit chain is one exec-mask branch per clause,
+    // each holding a saved mask in SGPRs that the grid search then spills)
+    bool ok = dir_ok(r.d.x);
+    ok &= dir_ok(r.d.y);
+    ok &= dir_ok(r.d.z);
+    ok &= org_ok(r.o.x);
+    ok &= org_ok(r.o.y);
+    ok &= org_ok(r.o.z);
+    return ok;
 }
 
 // RN(a / d) given y = RN(1/d), inside the guarded ranges.

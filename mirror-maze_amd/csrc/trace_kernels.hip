@@ -154,28 +154,121 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // Mirror-tail deferral (job.defer_from < 2^30): once at most defer_lanes of a
 // wave's 64 lanes still run -- past bounce_limit only paths that hit mirrors
 // continue (shaders.metal:306, `n < bounce_limit + mirror_hits`) -- those
-// lanes queue their path state and the wave takes a new chunk; k_trace_tail
-// then runs the queued tails 64 to a wave.  On C3 a
-// wave otherwise spends ~27 % of its bounce iterations on <= 12 live lanes
-// (scripts/grid_sim.c).  Samples are then staged per path and resolved by
-// k_resolve (the same operations in the same order as the fused resolve).
+// lanes queue their path state in their block's tail ring and the wave takes
+// a new chunk; the block's waves take 64 queued tails at a time as a chunk of
+// their own.  On C3 a wave otherwise spends ~27 % of its bounce iterations on
+// <= 12 live lanes (scripts/grid_sim.c).  Samples are then staged per path and
+// resolved by k_resolve (the same operations in the same order as the fused
+// resolve).
 
-// A deferred path's state into its reserved queue entry.
+// A deferred path's state into / out of queue record i (mm_launch.h TailQueue).
 __device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t i, const PathState& p, uint32_t slot) {
-    q.f(0)[i] = p.ori.x; q.f(1)[i] = p.ori.y; q.f(2)[i] = p.ori.z;
-    q.f(3)[i] = p.dir.x; q.f(4)[i] = p.dir.y; q.f(5)[i] = p.dir.z;
-    q.f(6)[i] = p.T.x; q.f(7)[i] = p.T.y; q.f(8)[i] = p.T.z;
-    q.f(9)[i] = p.L.x; q.f(10)[i] = p.L.y; q.f(11)[i] = p.L.z;
-    q.u(0)[i] = p.seed;
-    q.u(1)[i] = (uint32_t)p.n | ((uint32_t)p.mh << 16);
-    q.u(2)[i] = slot;
+    uint4* r = q.rec + 4u * (size_t)i;
+    r[0] = make_uint4(__float_as_uint(p.ori.x), __float_as_uint(p.ori.y), __float_as_uint(p.ori.z),
+                      __float_as_uint(p.dir.x));
+    r[1] = make_uint4(__float_as_uint(p.dir.y), __float_as_uint(p.dir.z), __float_as_uint(p.T.x),
+                      __float_as_uint(p.T.y));
+    r[2] = make_uint4(__float_as_uint(p.T.z), __float_as_uint(p.L.x), __float_as_uint(p.L.y),
+                      __float_as_uint(p.L.z));
+    r[3] = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, 0u);
+}
+
+__device__ __forceinline__ uint32_t tail_load(const TailQueue& q, uint32_t i, PathState& p) {
+    const uint4* r = q.rec + 4u * (size_t)i;
+    const uint4 a = r[0], b = r[1], c = r[2], d = r[3];
+    p.ori = F3{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
+    p.dir = F3{__uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)};
+    p.T = F3{__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x)};
+    p.L = F3{__uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w)};
+    p.seed = d.x;
+    p.n = (int)(d.y & 0xFFFFu);
+    p.mh = (int)(d.y >> 16);
+    return d.z;
 }
 
 __device__ __forceinline__ F3 path_value(const PathState& p) {
     return F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))};
 }
 
-template <bool kStats, bool kDefer, typename Q>
+// Block-local tail ring (kDefer): kTailRing entries per
+// block, payload in the queue's records blockIdx.x * kTailRing + slot.  LDS
+// words (static, at constant addresses -- every word of the ring's state that
+// lives in an SGPR across the bounce loop pushes a grid-search value into a
+// spill): ctl[0] = entries reserved, ctl[1] = entries claimed, ctl[2] = waves
+// past the global queue, then one turn word per slot.  Entry n lives in slot
+// n % kTailRing; its writer waits for turn == 2 * lap (the previous lap's
+// reader is done), writes the payload, sets 2 * lap + 1; its reader waits for
+// that, loads, sets 2 * lap + 2.  A writer reserves only entries whose
+// previous-lap entry is claimed and a reader claims only reserved entries, so
+// every wait is on an operation of a smaller entry number that is already
+// under way -- no cycle.  Only waves of one block (one CU) touch a ring:
+// workgroup-scope release / acquire order the payload, no L2 writeback or
+// invalidate.
+__device__ __forceinline__ uint32_t* ring_ctl() {
+    __shared__ uint32_t words[4 + kTailRing];
+    return words;
+}
+__device__ __forceinline__ uint32_t* ring_turn(uint32_t seq) { return ring_ctl() + 4 + (seq % kTailRing); }
+__device__ __forceinline__ uint32_t ring_lap(uint32_t seq) { return seq / kTailRing; }
+
+__device__ __forceinline__ uint32_t lds_ld(uint32_t* a) {
+    return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The executing lanes reserve consecutive entries: one LDS atomic by the
+// leader, no loop (a CAS loop nested in the bounce loop costs SGPRs the grid
+// search spills).  The leader adds only if the ring keeps kRingSlack free
+// entries: the block's other 15 waves may each add <= 16 concurrently, so a
+// reservation never passes `ring` unread entries.  false: no lane defers.
+constexpr uint32_t kRingSlack = 256;
+static_assert(kTailRing >= 2 * kRingSlack, "ring too small for the reservation slack");
+__device__ __forceinline__ bool ring_reserve(uint32_t& seq) {
+    uint32_t* ctl = ring_ctl();
+    const uint64_t m = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    uint32_t base = 0xFFFFFFFFu;
+    if (lane == leader) {
+        const uint32_t claimed = lds_ld(ctl + 1);
+        const uint32_t reserved = lds_ld(ctl + 0);  // read after claimed: reserved >= claimed
+        if (reserved + cnt - claimed + kRingSlack <= kTailRing)
+            base = __hip_atomic_fetch_add(ctl + 0, cnt, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    base = __shfl(base, (int)leader);
+    if (base == 0xFFFFFFFFu) return false;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    seq = base + (uint32_t)__popcll(m & lt);
+    return true;
+}
+
+// Leader lane: claim min(available, 64) entries if at least `need` are
+// reserved and not yet claimed; returns the count (0: none), first in `first`.
+__device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
+    uint32_t* ctl = ring_ctl();
+    uint32_t claimed = lds_ld(ctl + 1);
+    const uint32_t reserved = lds_ld(ctl + 0);  // read after claimed: reserved >= claimed
+    const uint32_t avail = reserved - claimed;
+    if (avail < need) return 0;
+    const uint32_t k = min(avail, 64u);
+    if (!__hip_atomic_compare_exchange_strong(ctl + 1, &claimed, claimed + k, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP))
+        return 0;
+    first = claimed;
+    return k;
+}
+
+// Every wait is bounded (~0.1 s): a protocol bug ends the launch with error
+// bit 2 set rather than a grid that never drains.
+constexpr uint32_t kRingSpin = 1u << 21;
+__device__ __forceinline__ void ring_wait(uint32_t* turn, uint32_t want, uint32_t* err) {
+    for (uint32_t i = 0; lds_ld(turn) != want; ++i) {
+        if (i == kRingSpin) { atomicOr(err, 2u); return; }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
                                                      float4* __restrict__ samples, unsigned long long* stats,
                                                      uint32_t* err, uint32_t* work) {
@@ -212,23 +305,11 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             p.n = 0;
             p.mh = 0;
             bool overflow = false;
-            uint32_t qi = 0;
-            bool deferred = false;
-            if constexpr (kDefer)
-                deferred = bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c,
-                                               overflow, (int)job.defer_from, job.defer_lanes, job.tail.count,
-                                               job.tail.cap, &qi);
-            else
-                bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
-                                    1 << 30, 0u);
+            bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow);
             if (overflow) atomicOr(err, 1u);
-            const uint32_t slot = fr * n_paths + path;
-            if (deferred) tail_store(job.tail, qi, p, slot);
-            if (!deferred) {
-                s = path_value(p);
-                if (!job.fuse) samples[slot] = make_float4(s.x, s.y, s.z, 0.0f);
-                paths++;
-            }
+            s = path_value(p);
+            if (!job.fuse) samples[fr * n_paths + path] = make_float4(s.x, s.y, s.z, 0.0f);
+            paths++;
         }
         if (job.fuse) resolve_in_wave(job, s, path, valid, job.out + (size_t)fr * job.w * job.h);
     }
@@ -252,63 +333,133 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     return chunks;
 }
 
-// The deferred tails: waves take 64 queued paths at a time and finish them.
+// With tail deferral (kDefer): a wave's next chunk is 64 queued
+// tails from its block's ring when there are that many, else 64 new paths
+// from the global queue; once that is out, whatever the ring still holds
+// (deferral off, so the block drains), until every wave of the block is past
+// the global queue and every entry is claimed.  A tail chunk runs the same
+// bounce loop as a new one (and may defer again) -- one copy of the loop in
+// the kernel.
 template <bool kStats, typename Q>
-__device__ __forceinline__ uint32_t tail_body(const DevScene& sc, const Q& q, const TileJob& job,
-                                              float4* __restrict__ samples, unsigned long long* stats,
-                                              uint32_t* err, uint32_t*) {
-    const TailQueue& tq = job.tail;
-    const uint32_t n = min(tq.count[0], tq.cap);  // reservations past cap were not used
+__device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, const Q& q, const TileJob& job,
+                                              float4* __restrict__ samples, unsigned long long* stats, uint32_t* err,
+                                              uint32_t* work) {
+    const uint32_t spp = job.e.spp;
+    const uint32_t n_paths = job.w * job.h * spp;
+    const uint32_t cpf = (n_paths + 63u) / 64u;
+    const uint32_t n_queue = cpf * 64u * job.n_frames;
     const uint32_t lane = threadIdx.x & 63u;
+    const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
+    const TailQueue& tq = job.tail;
     Counters c;
     ScratchStack stack;
-    uint32_t paths = 0, chunks = 0;
-#ifdef MM_TAIL_TIMELINE
-    uint32_t wave_iters = 0;
+    uint32_t paths = 0, chunks = 0, idle = 0;
+    int defer_from = (int)job.defer_from;  // 2^30 (off) once the global queue is out
+#ifdef MM_RING_CLOCKS  // diagnostics: per wave (main chunks, tail chunks, ring waits, drain idle) wall clock
+    uint64_t rc_main = 0, rc_tail = 0, rc_idle = 0;
+    uint64_t rc_t0 = 0;
 #endif
     for (;;) {
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(tq.count + 1, 64u);
-        const uint32_t base = __builtin_amdgcn_readfirstlane(b);
-        if (base >= n) break;
-        ++chunks;
-        const uint32_t i = base + lane;
-#ifdef MM_TAIL_TIMELINE
-        int lane_bounces = 0;
+#ifdef MM_RING_CLOCKS
+        rc_t0 = wall_clock64();
 #endif
-        if (i < n) {
-            PathState p;
-            p.ori = F3{tq.f(0)[i], tq.f(1)[i], tq.f(2)[i]};
-            p.dir = F3{tq.f(3)[i], tq.f(4)[i], tq.f(5)[i]};
-            p.T = F3{tq.f(6)[i], tq.f(7)[i], tq.f(8)[i]};
-            p.L = F3{tq.f(9)[i], tq.f(10)[i], tq.f(11)[i]};
-            p.seed = tq.u(0)[i];
-            const uint32_t nm = tq.u(1)[i];
-            p.n = (int)(nm & 0xFFFFu);
-            p.mh = (int)(nm >> 16);
-            bool overflow = false;
-#ifdef MM_TAIL_TIMELINE
-            const int n0 = p.n;
+        uint32_t first = 0, k = 0, b = 0;
+        if (lane == 0) k = ring_claim(defer_from == (1 << 30) ? 1u : 64u, first);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (!k) {
+            if (defer_from == (1 << 30)) {
+                uint32_t done = 0;
+                if (lane == 0)
+                    done = lds_ld(ring_ctl() + 2) == (blockDim.x >> 6) && lds_ld(ring_ctl() + 0) == lds_ld(ring_ctl() + 1);
+                if (__builtin_amdgcn_readfirstlane(done)) break;
+                if (++idle == kRingSpin) {
+                    if (lane == 0) atomicOr(err, 2u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+#ifdef MM_RING_CLOCKS
+                rc_idle += wall_clock64() - rc_t0;
 #endif
-            bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
-                                1 << 30, 0u);
-#ifdef MM_TAIL_TIMELINE
-            lane_bounces = p.n - n0 + 1;
-#endif
-            if (overflow) atomicOr(err, 1u);
-            const F3 s = path_value(p);
-            samples[tq.u(2)[i]] = make_float4(s.x, s.y, s.z, 0.0f);
-            paths++;
+                continue;
+            }
+            if (lane == 0) b = atomicAdd(work, 64u);
+            if (__builtin_amdgcn_readfirstlane(b) >= n_queue) {
+                if (lane == 0)
+                    __hip_atomic_fetch_add(ring_ctl() + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                defer_from = 1 << 30;
+                continue;
+            }
         }
-#ifdef MM_TAIL_TIMELINE  // the wave's bounce iterations for this chunk: its lanes' maximum
-        for (int o = 32; o > 0; o >>= 1) lane_bounces = max(lane_bounces, __shfl_xor(lane_bounces, o));
-        wave_iters += (uint32_t)lane_bounces;
+        ++chunks;
+        PathState p;
+        uint32_t slot = 0;
+        bool live;
+        if (k) {  // queued tails
+            live = lane < k;
+            if (live) {
+                const uint32_t seq = __builtin_amdgcn_readfirstlane(first) + lane;
+                const uint32_t lap = ring_lap(seq);
+                ring_wait(ring_turn(seq), 2u * lap + 1u, err);
+                slot = tail_load(tq, blockIdx.x * kTailRing + seq % kTailRing, p);
+                // (the release waits for the loads above)
+                __hip_atomic_store(ring_turn(seq), 2u * lap + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {  // new paths
+            const uint32_t qc = __builtin_amdgcn_readfirstlane(b) >> 6;
+            const uint32_t fr = job.n_frames > 1 ? qc / cpf : 0u;
+            const uint32_t path = (qc - fr * cpf) * 64u + lane;
+            live = path < n_paths;
+            if (live) {
+                const uint32_t pix = path / spp, smp = path - pix * spp;
+                const uint32_t j = pix / job.w, i = pix - j * job.w;
+                const uint32_t px = job.x0 + i, py = job.y0 + j * job.y_stride;
+                p.seed = seed_tile(py * job.view_w + px, smp, job.e.frame + fr);
+                p.dir = jitter(primary_dir(job.u, px, py), p.seed);
+                p.ori = ori;
+                p.T = F3{1.0f, 1.0f, 1.0f};
+                p.L = F3{0.0f, 0.0f, 0.0f};
+                p.n = 0;
+                p.mh = 0;
+                slot = fr * n_paths + path;
+            }
+        }
+        if (live) {
+            bool overflow = false;
+            uint32_t seq = 0;
+            const bool deferred = bounce_loop_r<kStats>(
+                sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
+                defer_from, job.defer_lanes, [&]() { return ring_reserve(seq); });
+            if (overflow) atomicOr(err, 1u);
+            if (deferred) {
+                const uint32_t lap = ring_lap(seq);
+                ring_wait(ring_turn(seq), 2u * lap, err);
+                tail_store(tq, blockIdx.x * kTailRing + seq % kTailRing, p, slot);
+                __hip_atomic_store(ring_turn(seq), 2u * lap + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                const F3 s = path_value(p);
+                samples[slot] = make_float4(s.x, s.y, s.z, 0.0f);
+                paths++;
+            }
+        }
+#ifdef MM_RING_CLOCKS
+        {
+            const uint64_t dt = wall_clock64() - rc_t0;
+            if (k) rc_tail += dt; else rc_main += dt;
+        }
 #endif
     }
-    if (kStats) flush_stats(stats, c, paths);
-#ifdef MM_TAIL_TIMELINE
-    return wave_iters;
+#ifdef MM_RING_CLOCKS
+    if (job.wave_ts && lane == 0) {
+        const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) + 16384u;
+        if (wid < job.wave_ts_cap) {
+            job.wave_ts[4 * wid + 0] = rc_main;
+            job.wave_ts[4 * wid + 1] = rc_tail;
+            job.wave_ts[4 * wid + 2] = chunks;
+            job.wave_ts[4 * wid + 3] = rc_idle;
+        }
+    }
 #endif
+    if (kStats) flush_stats(stats, c, paths);
     return chunks;
 }
 
@@ -408,10 +559,9 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
 // persistent kernels (counter[0] = next item, counter[1] = waves done; the
 // last wave to finish re-zeroes the words, so the next launch needs no memset
 // -- a fill kernel queued between two frames on another stream would wait for
-// free CUs and serialise overlapping frames).  `extra` (or null): a third word
-// the last wave also clears (the tail queue's entry count).
+// free CUs and serialise overlapping frames).
 __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chunks, unsigned long long t_entry,
-                                                uint32_t* counter, uint32_t* extra) {
+                                                uint32_t* counter) {
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (wid < job.wave_ts_cap) {
@@ -431,7 +581,6 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
         if (atomicAdd(counter + 1, 1u) == total - 1) {
             atomicExch(counter, 0u);
             atomicExch(counter + 1, 0u);
-            if (extra) atomicExch(extra, 0u);
         }
     }
 }
@@ -443,25 +592,22 @@ template <bool kStats, int kLds, int kForm, bool kDefer>
 __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {
+    if constexpr (kDefer) {  // the block's tail ring: counters and turn words zero
+        for (uint32_t i = threadIdx.x; i < 4u + kTailRing; i += blockDim.x) ring_ctl()[i] = 0u;
+        __syncthreads();
+    }
 #ifdef MM_PHASE_CLOCKS
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
 #else
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
 #endif
     const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
-        return wavepersist_body<kStats, kDefer>(sc, q, job, samples, stats, err, work);
+        if constexpr (kDefer)
+            return wavepersist_ring_body<kStats>(sc, q, job, samples, stats, err, work);
+        else
+            return wavepersist_body<kStats>(sc, q, job, samples, stats, err, work);
     });
-    persistent_exit(job, chunks, t_entry, work, nullptr);
-}
-
-template <bool kStats, int kLds, int kForm>
-__global__ __launch_bounds__(1024, 8) void k_trace_tail(DevScene sc, TileJob job, float4* __restrict__ samples,
-                                                        unsigned long long* stats, uint32_t* err) {
-    const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
-    const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
-        return tail_body<kStats>(sc, q, job, samples, stats, err, nullptr);
-    });
-    persistent_exit(job, chunks, t_entry, job.tail.count + 1, job.tail.count);
+    persistent_exit(job, chunks, t_entry, work);
 }
 
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
@@ -493,25 +639,14 @@ template <int kLds, int kForm, bool kDefer>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        hipStream_t s) {
-    const size_t lds = wavepersist_lds_bytes(sc, kLds);
+    const size_t lds = wavepersist_lds_bytes(sc, kLds);  // (+ the tail ring's static LDS when kDefer)
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm, kDefer>
                             : k_trace_wavepersist<false, kLds, kForm, kDefer>;
     const uint32_t grid =
         persistent_grid(kern, lds, job.reserve_cus, (uint64_t)job.w * job.h * job.e.spp * job.n_frames);
     if (!grid) return hipErrorInvalidValue;
+    if (kDefer && (uint64_t)grid * kTailRing > job.tail.cap) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, s, sc, job, samples, stats, err, work);
-    return hipGetLastError();
-}
-
-template <int kLds, int kForm>
-static hipError_t launch_tail_t(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
-                                uint32_t* err, bool count_stats, hipStream_t s) {
-    const size_t lds = wavepersist_lds_bytes(sc, kLds);
-    auto kern = count_stats ? k_trace_tail<true, kLds, kForm> : k_trace_tail<false, kLds, kForm>;
-    // the queue length is known on the device only: a full resident grid (each wave drains 64 at a time)
-    const uint32_t grid = persistent_grid(kern, lds, job.reserve_cus, ~0ull >> 1);
-    if (!grid) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, s, sc, job, samples, stats, err);
     return hipGetLastError();
 }
 
@@ -548,15 +683,6 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
     if (lds_mode == L && form == F && !defer)                                                                \
         return launch_wavepersist_t<L, F, false>(sc, job, samples, stats, err, work, count_stats, s);
     MM_WP_INSTANCES(MM_WP)
-#undef MM_WP
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_trace_tail(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
-                             uint32_t* err, bool count_stats, int lds_mode, int form, hipStream_t s) {
-#define MM_WP(L, F) \
-    if (lds_mode == L && form == F) return launch_tail_t<L, F>(sc, job, samples, stats, err, count_stats, s);
-    MM_DEFER_INSTANCES(MM_WP)
 #undef MM_WP
     return hipErrorInvalidValue;
 }

@@ -28,9 +28,13 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--opt", action="append", default=[], help="MM_OPT key:value (repeatable)")
     a = ap.parse_args()
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
     r = Renderer(0)
+    for kv in a.opt:
+        k, v = kv.split(":")
+        r.set_option(int(k), int(v))
     r.upload_scene(Scene.build(maze_n, 0))
     u = default_uniform(W, H, 0)
     ts = torch.zeros((65536, 4), dtype=torch.int64, device="cuda")

@@ -34,8 +34,8 @@ def test_c3_bench_path_two_whole_frames(gpu, opts):
     """C3 as bench.py renders it: MM_PIPE_AUTO (the grid search), consecutive
     frames in ONE mm_trace_tile_frames launch, every pixel of both 1920x1080
     frames (2 x 137 M closest-hit queries) vs the oracle -- with mirror-tail
-    deferral (bench.py's 10-frame launches are past MM_OPT_DEFER_MIN; this
-    2-frame launch needs the threshold lowered) and without it."""
+    deferral through the block-local tail rings (the default past
+    MM_OPT_DEFER_MIN = 2^24 paths, as in bench.py's launches) and without it."""
     from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 

@@ -116,8 +116,10 @@ PIPES = {
     "grid": (1, {7: 11}, False),
     "grid-nofuse": (1, {7: 11, 12: 0}, False),
     "grid-nodefer": (1, {21: 0}, False),
-    "grid-defer16": (1, {22: 0}, False),                     # tail deferral on any launch size
+    "grid-defer": (1, {22: 0}, False),                       # tail deferral (32 lanes) on any launch size
+    "grid-defer16": (1, {21: 16, 22: 0}, False),
     "grid-defer63": (1, {21: 63, 22: 0}, False),
+    "grid-defer64": (1, {21: 64, 22: 0}, False),             # every path at bounce 1: tail rings run full
     "bvh-lean-defer32": (1, {7: 7, 21: 32, 22: 0}, True),
     "bvh-lean-ldsrects": (1, {7: 7}, True),
     "bvh-lean-globalrecs": (1, {7: 7, 8: 0}, True),
@@ -130,7 +132,7 @@ PIPES = {
     "bvh-li-dict": (1, {7: 5, 20: 2}, True),
     "bvh-ifif-ldsrects": (1, {7: 0}, True),
     "bvh-ifif-lds": (1, {7: 0, 8: 0}, True),
-    "wavefront": (2, {}, False),                             # the compacted mirror-tail queue always on
+    "wavefront": (2, {}, False),                             # mirror-tail deferral always on
     "wavefront-global": (2, {1: 0}, False),
 }
 
@@ -174,8 +176,8 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
     ren.close()
 
 
-@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-nodefer", "grid-defer16", "bvh-lean-ldsrects",
-                                  "bvh-li-dict", "mega-lds", "wavefront"])
+@pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-nodefer", "grid-defer", "grid-defer64",
+                                  "bvh-lean-ldsrects", "bvh-li-dict", "mega-lds", "wavefront"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
