@@ -88,7 +88,7 @@ struct mm_ctx {
     bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
-    int opt_defer = 32;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off)
+    int opt_defer = -1;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off, -1 auto)
     uint32_t opt_defer_min = 1u << 24;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
@@ -734,7 +734,10 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     }
     // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run from block-local rings; built for
     // the grid search and the lean BVH form with records in LDS (other forms run without it)
-    const bool defer = persist && (c->opt_defer > 0 || wave) && wavepersist_defer_built(mode, form) &&
+    // (auto: with the whole search structure in LDS -- the grid image, or BVH nodes + compact records; the N=64
+    // scene's records read through L1/L2 gain nothing from it: C5 frame 231.4 vs 227.7 ms without)
+    const bool defer_on = c->opt_defer > 0 || (c->opt_defer < 0 && (mode == 11 || mode == 3));
+    const bool defer = persist && (defer_on || wave) && wavepersist_defer_built(mode, form) &&
                        (wave || (uint64_t)w * h * e->spp * n_frames >= c->opt_defer_min);
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
     const bool fuse = persist && !defer && c->opt_fuse && 64 % e->spp == 0;

@@ -215,13 +215,12 @@ __device__ __forceinline__ uint32_t lds_ld(uint32_t* a) {
     return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The executing lanes reserve consecutive entries: one LDS atomic by the
-// leader, no loop (a CAS loop nested in the bounce loop costs SGPRs the grid
-// search spills).  The leader adds only if the ring keeps kRingSlack free
-// entries: the block's other 15 waves may each add <= 16 concurrently, so a
-// reservation never passes `ring` unread entries.  false: no lane defers.
-constexpr uint32_t kRingSlack = 256;
-static_assert(kTailRing >= 2 * kRingSlack, "ring too small for the reservation slack");
+// The executing lanes reserve consecutive entries: ONE compare-and-swap by the
+// leader, no retry loop (a loop nested in the bounce loop costs SGPRs the grid
+// search then spills).  It fails if the ring lacks room for them or another
+// wave of the block reserved in between; then no lane defers and the wave
+// tries again at its next bounce.  Exact: `reserved - claimed` never passes
+// kTailRing.
 __device__ __forceinline__ bool ring_reserve(uint32_t& seq) {
     uint32_t* ctl = ring_ctl();
     const uint64_t m = __ballot(1);
@@ -231,9 +230,11 @@ __device__ __forceinline__ bool ring_reserve(uint32_t& seq) {
     uint32_t base = 0xFFFFFFFFu;
     if (lane == leader) {
         const uint32_t claimed = lds_ld(ctl + 1);
-        const uint32_t reserved = lds_ld(ctl + 0);  // read after claimed: reserved >= claimed
-        if (reserved + cnt - claimed + kRingSlack <= kTailRing)
-            base = __hip_atomic_fetch_add(ctl + 0, cnt, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint32_t reserved = lds_ld(ctl + 0);  // read after claimed: reserved >= claimed
+        if (reserved + cnt - claimed <= kTailRing &&
+            __hip_atomic_compare_exchange_strong(ctl + 0, &reserved, reserved + cnt, __ATOMIC_ACQ_REL,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            base = reserved;
     }
     base = __shfl(base, (int)leader);
     if (base == 0xFFFFFFFFu) return false;

@@ -34,6 +34,7 @@ VARIANTS = {
     "nodefer": (1, {21: 0}),
     "defer8": (1, {21: 8}),
     "defer16": (1, {21: 16}),
+    "defer24": (1, {21: 24}),
     "defer32": (1, {21: 32}),
     "defer48": (1, {21: 48}),
     "defer64": (1, {21: 64}),       # every path deferred at bounce 1: the tail rings run the rest
