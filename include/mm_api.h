@@ -134,9 +134,10 @@ int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
 /* Pipeline selection for mm_trace_tile (MM_PIPE_AUTO picks the fastest). */
 #define MM_PIPE_AUTO       0
 #define MM_PIPE_MEGAKERNEL 1   /* bounce loop in-kernel (MM_OPT_PERSIST picks the kernel) */
-#define MM_PIPE_WAVEFRONT  2   /* the wave-persistent kernel with the compacted mirror-tail queue always on
-                                  (MM_OPT_DEFER, 16 lanes unless set): the bounce loop's divergent tail
-                                  continues in a dense second kernel.  The round-1 fully flattened pipeline
+#define MM_PIPE_WAVEFRONT  2   /* the wave-persistent kernel with the mirror-tail deferral always on
+                                  (MM_OPT_DEFER, 32 lanes unless set): a wave's divergent tail is parked
+                                  in its block's ring and resumed 64 paths at a time, densely.  The round-1
+                                  fully flattened pipeline
                                   (SoA state in HBM, one extend/shade launch pair per bounce) measured
                                   ~45 ms vs 5.7 ms per C3 frame and was retired (DESIGN.md §4,
                                   profiles/r02_wavefront_pmc.txt) */
