@@ -263,7 +263,7 @@ def main():
     u = default_uniform(W, H, 0)
 
     # rows r, r+world, ... (mirror_maze/dist.py); pad so every rank sends the same shape
-    from mirror_maze.dist import FrameGatherer, row_shard, rows_max
+    from mirror_maze.dist import BatchGatherer, FrameGatherer, row_shard, rows_max
 
     y0, y_stride, my_rows = row_shard(H, world, rank)
     if args.emulate_ranks > 1 and world == 1:
@@ -280,10 +280,14 @@ def main():
     fb_max = (min(args.batch, max(args.steps, args.warmup, 8)) if args.batch > 0 else 8) if batchable else 1
     # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,
     # so the next launch never waits on this batch's own gathers
+    asm_stream = torch.cuda.Stream(dev) if distributed else None
     gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf, dtype=fdt,
-                              slots=max(2, len(rens), 2 * fb_max if fb_max > 1 else 0),
-                              assembly_stream=torch.cuda.Stream(dev))
+                              slots=max(2, len(rens)), assembly_stream=asm_stream)
                 if distributed else None)
+    # multi-frame launches: ONE gather per launch (its frames all finish together)
+    bgather = (BatchGatherer((rows_max(H, world), W, 4), H, dev, fb_max, out=frame_buf, dtype=fdt, slots=2,
+                             assembly_stream=asm_stream)
+               if distributed and fb_max > 1 else None)
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=fdt, device=dev) for _ in rens]
     # float tiles the trace writes when the delivered frame is RGBA8 (one per context)
     ftiles = [torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev) for _ in rens] if rgba8 else None
@@ -333,13 +337,14 @@ def main():
         with torch.cuda.stream(streams[slot]):
             _, st = rens[slot].trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), n, 0, y0, W, my_rows,
                                                  y_stride=y_stride, out=batch_buf[:n], stats=stats)
-            if gatherer:
+            if bgather:
+                tl = bgather.tiles(n)
                 for f in range(n):
                     if rgba8:
-                        rens[slot].quantize(batch_buf[f], out=gatherer.tile()[:my_rows])
+                        rens[slot].quantize(batch_buf[f], out=tl[f][:my_rows])
                     else:
-                        gatherer.tile()[:my_rows].copy_(batch_buf[f])
-                    gatherer.put()
+                        tl[f][:my_rows].copy_(batch_buf[f])
+                bgather.put(n)
             elif rgba8:  # every frame delivered in RGBA8
                 for f in range(n):
                     rens[slot].quantize(batch_buf[f], out=batch_buf8[f])
@@ -356,7 +361,7 @@ def main():
             for li, n in enumerate(launch_sizes(count, per)):
                 step_batch(k0 + i, frame0 + i, n, slot=li % active[0])
                 i += n
-            if not gatherer and count > 0:  # the last frame, for frame_buf
+            if not bgather and count > 0:  # the last frame, for frame_buf
                 sl = last[0]
                 with torch.cuda.stream(streams[sl]):
                     tiles1[sl][:my_rows].copy_(batch_bufs8[sl][n - 1] if rgba8 else batch_bufs[sl][n - 1])
@@ -374,11 +379,16 @@ def main():
                 tiles1[0].copy_(acc_tile[:H])
                 last[0] = 0
 
+    def flush_gathers():
+        if bgather:
+            bgather.flush()
+        if gatherer:
+            gatherer.flush()
+
     def drain():
         if acc_tile is not None:
             gather_accumulated()
-        if gatherer:
-            gatherer.flush()
+        flush_gathers()
         torch.cuda.synchronize(dev)
         if not gatherer:
             frame_buf.copy_(tiles1[last[0]])
@@ -436,8 +446,7 @@ def main():
                 progress(f"timed frame {i + 1}/{args.steps} queued")
     if acc_tile is not None:
         gather_accumulated()  # C5: one gather of the accumulated frame, inside the timed region
-    if gatherer:
-        gatherer.flush()  # the last frames' gathers + assembly are inside the timed region
+    flush_gathers()  # the last frames' gathers + assembly are inside the timed region
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()

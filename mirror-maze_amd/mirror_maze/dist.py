@@ -6,7 +6,9 @@ renders rows r, r+N, r+2N, ...), which balances the very uneven per-row cost
 (pixel, sample, frame) so the N-GPU image equals the 1-GPU image bit for bit.
 At frame end one collective moves every tile to rank 0: torch.distributed's
 gather (RCCL send/recv over xGMI with the "nccl" backend; gloo on CPU for
-tests), then a de-interleave on rank 0.
+tests), then a de-interleave on rank 0.  FrameGatherer pipelines one gather
+per frame; BatchGatherer issues one gather per multi-frame launch (bench.py's
+default issue mode: the launch's frames all finish together).
 """
 from __future__ import annotations
 
@@ -147,3 +149,100 @@ class FrameGatherer:
             self.out.copy_(frame)
         if self.on_frame is not None:
             self.on_frame(k, self.out)
+
+
+class BatchGatherer:
+    """One gather per multi-frame launch.
+
+    The frames of one ``mm_trace_tile_frames`` launch all finish when the
+    launch does, so gathering them one by one buys no earlier delivery -- only
+    n collectives' fixed latency where one would do.  ``tiles(n)`` hands out
+    the (n, rows_max, W, C) slice of a slot buffer (completing the gather that
+    last used the slot) for the launch's frames; ``put(n)`` issues ONE
+    asynchronous gather of the whole slice (every rank passes the same n: the
+    launch sizes are deterministic); rank ``dst`` de-interleaves frame by frame
+    into ``out`` and calls ``on_frame(k, frame)`` in frame order when the slot
+    is reused or on ``flush()``.  ``slots`` buffers rotate (2: the next launch's
+    frames are converted while this launch's gather runs)."""
+
+    def __init__(self, shape, height: int, device, max_frames: int, dst: int = 0, group=None, out=None,
+                 slots: int = 2, on_frame=None, assembly_stream=None, dtype=None):
+        import torch
+        import torch.distributed as dist
+
+        self.height, self.dst, self.group, self.out = height, dst, group, out
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.slots, self.max_frames = slots, max_frames
+        self.on_frame = on_frame
+        dtype = torch.float32 if dtype is None else dtype
+        bshape = (max_frames,) + tuple(shape)
+        self.tiles_ = [torch.zeros(bshape, dtype=dtype, device=device) for _ in range(slots)]
+        self.bufs = ([[torch.empty(bshape, dtype=dtype, device=device) for _ in range(self.world)]
+                      for _ in range(slots)] if self.rank == dst else [None] * slots)
+        self.k = 0         # frames issued so far
+        self.launch = 0    # gathers issued so far
+        self.pending = [None] * slots   # (first frame, n, Work) per slot
+        self.asm = assembly_stream
+        self.asm_done = [None] * slots
+
+    def tiles(self, n: int):
+        """The (n, rows_max, W, C) buffer the next launch's frames go into."""
+        if not (1 <= n <= self.max_frames):
+            raise ValueError(f"batch of {n} frames outside 1..{self.max_frames}")
+        slot = self.launch % self.slots
+        self._finish(slot)
+        return self.tiles_[slot][:n]
+
+    def put(self, n: int):
+        """Issue the gather of the n frames just written into ``tiles(n)``."""
+        import torch.distributed as dist
+
+        slot = self.launch % self.slots
+        if self.asm_done[slot] is not None:
+            import torch
+
+            torch.cuda.current_stream().wait_event(self.asm_done[slot])
+            self.asm_done[slot] = None
+        recv = [b[:n] for b in self.bufs[slot]] if self.bufs[slot] is not None else None
+        work = dist.gather(self.tiles_[slot][:n], recv, dst=self.dst, group=self.group, async_op=True)
+        self.pending[slot] = (self.k, n, work)
+        self.k += n
+        self.launch += 1
+
+    def flush(self):
+        """Complete every outstanding gather (oldest first); returns ``out``."""
+        for i in range(self.slots):
+            self._finish((self.launch + i) % self.slots)
+        return self.out
+
+    def _finish(self, slot):
+        p = self.pending[slot]
+        if p is None:
+            return
+        self.pending[slot] = None
+        k, n, work = p
+        work.wait()
+        if self.rank != self.dst:
+            return
+        if self.asm is None:
+            self._assemble(k, n, slot)
+            return
+        import torch
+
+        with torch.cuda.stream(self.asm):
+            work.wait()
+            self._assemble(k, n, slot)
+            ev = torch.cuda.Event()
+            ev.record(self.asm)
+            self.asm_done[slot] = ev
+
+    def _assemble(self, k, n, slot):
+        for f in range(n):
+            frame = assemble([b[f] for b in self.bufs[slot]], self.height)
+            if self.out is None:
+                self.out = frame.clone()
+            else:
+                self.out.copy_(frame)
+            if self.on_frame is not None:
+                self.on_frame(k + f, self.out)

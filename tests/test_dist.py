@@ -155,3 +155,69 @@ def test_row_shard_covers_every_row_once():
                 seen += [y0 + i * st for i in range(n)]
                 assert n <= rows_max(H, world)
             assert sorted(seen) == list(range(H))
+
+
+def _worker_batched(rank, world, port, H, W, q, sizes):
+    """Frames in launches of `sizes` frames, one BatchGatherer gather per launch
+    (bench.py's multi-frame path); RGBA8 tiles as bench.py delivers them."""
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo))
+    sys.path.insert(0, str(repo / "mirror-maze_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+
+    from mirror_maze import Scene, default_uniform, make_ext
+    from mirror_maze.dist import BatchGatherer, row_shard, rows_max
+    from mirror_maze.io import quantize
+    from oracle.oracle import Oracle
+
+    s = Scene.build(10, 0)
+    o = Oracle.from_scene(s)
+    u = default_uniform(W, H, 0)
+    y0, stride, rows = row_shard(H, world, rank)
+    frames = {}
+    g = BatchGatherer((rows_max(H, world), W, 4), H, "cpu", max(sizes), dtype=torch.uint8,
+                      on_frame=lambda k, fr: frames.__setitem__(k, fr.numpy().copy()))
+    f0 = 0
+    for n in sizes:
+        tl = g.tiles(n).numpy()
+        for f in range(n):
+            ft = np.zeros((rows, W, 4), dtype=np.float32)
+            o.trace_tile(u, make_ext(2, 3, 15, frame=f0 + f), 0, y0, W, rows, y_stride=stride, out=ft)
+            tl[f, :rows] = quantize(ft)
+        g.put(n)
+        f0 += n
+    out = g.flush()
+    if rank == 0:
+        assert sorted(frames) == list(range(f0)) and np.array_equal(out.numpy(), frames[f0 - 1])
+        q.put(np.stack([frames[k] for k in range(f0)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sizes", [(2, (3, 3, 2)), (3, (4, 1))])
+def test_gloo_batch_gather_per_launch(world, sizes):
+    from mirror_maze import Scene, default_uniform, make_ext
+    from mirror_maze.io import quantize
+    from oracle.oracle import Oracle
+
+    H, W = 11, 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_batched, args=(r, world, port, H, W, q, sizes)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    o = Oracle.from_scene(Scene.build(10, 0))
+    assert frames.shape == (sum(sizes), H, W, 4)
+    for f in range(sum(sizes)):
+        ref, _ = o.trace_tile(default_uniform(W, H, 0), make_ext(2, 3, 15, frame=f), 0, 0, W, H)
+        assert frames[f].dtype == np.uint8 and np.array_equal(frames[f], quantize(ref)), f
