@@ -36,7 +36,9 @@ VARIANTS = {
     "defer16": (1, {21: 16}),
     "defer24": (1, {21: 24}),
     "defer32": (1, {21: 32}),
+    "defer40": (1, {21: 40}),
     "defer48": (1, {21: 48}),
+    "defer56": (1, {21: 56}),
     "defer64": (1, {21: 64}),       # every path deferred at bounce 1: the tail rings run the rest
     "defer-min0": (1, {22: 0}),     # deferral on launches of any size
     "wave": (2, {}),
