@@ -92,7 +92,7 @@ def parse():
     p.add_argument("--contexts", type=int, default=0,
                    help="renderer contexts (one stream each) that consecutive frames alternate over; "
                         "0 = 1 on one GPU, 2 when the frame is split over ranks")
-    p.add_argument("--batch", type=int, default=16,
+    p.add_argument("--batch", type=int, default=32,
                    help="frames per launch at most (mm_trace_tile_frames: the frames share one work queue, so "
                         "the launch's drain and its tail kernel are paid once per launch, not per frame); 1 = one "
                         "frame per launch (then --contexts applies); 0 = time 1 context / 2 contexts / batches of "
