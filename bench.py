@@ -242,8 +242,8 @@ def main():
     scene = Scene.build(maze_n, 0)
     # Issue modes.  Every launch ends in a ~0.4 ms tail in which the last waves
     # finish their last chunks (profiles/r01_timeline_probe.txt) -- 4 % of a
-    # C3 frame, 25 % of a rank's frame at N = 8.  Default (--batch 8): frames
-    # are independent, so up to 8 consecutive frames share ONE launch's work
+    # C3 frame, 25 % of a rank's frame at N = 8.  Default (--batch 32): frames
+    # are independent, so up to 32 consecutive frames share ONE launch's work
     # queue (mm_trace_tile_frames) and the tail is paid once per launch.
     # --batch 1: one frame per launch, optionally alternating over two
     # renderer contexts on their own streams so frame k+1's blocks fill the
