@@ -71,3 +71,12 @@ def test_errors_are_codes_not_crashes():
     assert L.mm_trace_chunks(None, None, None, 0) == _lib.MM_ERR_INVALID
     assert L.mm_sync(None) == _lib.MM_ERR_INVALID
     assert L.mm_last_error(None) == b"null context"
+
+
+def test_integration_rust_binding_covers_the_declared_surface():
+    """INTEGRATION.md's extern "C" blocks name every declared function (the
+    binding a maintainer adds to the reference), and nothing undeclared."""
+    txt = (REPO / "INTEGRATION.md").read_text()
+    bound = set(re.findall(r"pub fn (mm_[a-z_0-9]+)\s*\(", txt))
+    declared = _declared_functions() - {"mm_layout_ok"}
+    assert bound == declared, (declared - bound, bound - declared)
