@@ -104,8 +104,9 @@ int  mm_quantize_rgba8(mm_ctx* ctx, const float* rgba_dev, uint8_t* rgba8_dev, u
 
 /* ---- throughput mode: offline renderer ------------------------------------
  * Renders pixels (x0 + i, y0 + j*y_stride), 0<=i<w, 0<=j<h, of the frame
- * uni->view_w x uni->view_h with ext->spp samples each, ext->bounce_limit /
- * ext->mirror_limit, RNG keyed on (pixel, sample, ext->frame) so any tiling
+ * uni->view_w x uni->view_h with ext->spp samples each (1..4096),
+ * ext->bounce_limit / ext->mirror_limit (0..32767; MM_ERR_INVALID otherwise),
+ * RNG keyed on (pixel, sample, ext->frame) so any tiling
  * over any number of GPUs reproduces the 1-GPU image bit for bit.
  * out_dev: caller DEVICE pointer to w*h float4 (row-major over (j,i));
  * alpha = 1 (or, with MM_EXT_ACCUMULATE, += the frame value, alpha += 1).

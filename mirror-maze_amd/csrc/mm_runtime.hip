@@ -715,6 +715,9 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     const uint32_t W = (uint32_t)u->view_w, H = (uint32_t)u->view_h;
     if (w == 0 || h == 0 || y_stride == 0 || e->spp == 0 || e->spp > 4096)
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: empty tile or bad spp");
+    // the tail records pack bounces | mirror hits << 16 (trace_kernels.hip tail_store)
+    if (e->bounce_limit > 32767 || e->mirror_limit > 32767)
+        return fail(c, MM_ERR_INVALID, "mm_trace_tile: bounce or mirror limit above 32767");
     if ((uint64_t)x0 + w > W || (uint64_t)y0 + (uint64_t)(h - 1) * y_stride >= H)
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: tile outside the frame");
     HIPC(c, hipSetDevice(c->device));

@@ -439,3 +439,20 @@ def test_bench_issue_mode_calibration(gpu):
         lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
         assert len(lines) == 1, r.stdout
         assert check(json.loads(lines[0])), lines[0]
+
+
+@pytest.mark.gpu
+def test_trace_tile_rejects_limits_beyond_the_packed_state(gpu):
+    """Bounce / mirror limits above 32767 would overflow the tail records'
+    bounces | mirror hits << 16 word: an error code, not a wrong image."""
+    from mirror_maze import Renderer, default_uniform, make_ext
+    from mirror_maze._lib import MMError
+
+    u = default_uniform(64, 32, 0)
+    with Renderer(0) as r:
+        r.upload_scene(_scene(10))
+        for bl, ml in ((40000, 8), (8, 40000)):
+            with pytest.raises(MMError):
+                r.trace_tile(u, make_ext(1, bl, ml), 0, 0, 4, 4)
+        img, _ = r.trace_tile(u, make_ext(1, 32767, 8), 0, 0, 4, 4)  # the bound itself is accepted
+        assert img.shape == (4, 4, 4)
