@@ -172,17 +172,17 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     uint32_t bk = 0xFFFFFFFFu;
     uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
     for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect<kSlow>(gv.recs, geo, g.glob[j], r, best, bk, tie);
-    // The walk starts in the cell of the ray's point at t = 1/16, not at the
+    // The walk starts in the cell of the ray's point at t = 3/32, not at the
     // origin: a rect of A has a > 0.1, so the cells the ray occupies only for
-    // t < 1/16 hold nothing it can return, and the rounding of the start
+    // t < 3/32 hold nothing it can return, and the rounding of the start
     // point (a few ulp of C) is covered by the eps-widened lists as the
     // crossing times are.  A bounce origin lies on a wall, i.e. within eps of
     // a cell face; from the origin the walk would start on the far side of
     // that face in about half the cases and test a cell the ray never enters
-    // (C3 3.40 -> 3.37 ms/frame, C5 scene 7.20 -> 7.05, bit-identical;
-    // profiles/r02_ab_start_cell.txt).  The crossing times stay those of the
-    // origin.
-    const float s0 = 0.0625f;
+    // (t = 1/16: C3 3.40 -> 3.37 ms/frame, C5 scene 7.20 -> 7.05; 3/32: a
+    // further 1.3 % / 1.4 %; bit-identical; profiles/r02_ab_start_cell.txt).
+    // The crossing times stay those of the origin.
+    const float s0 = 0.09375f;
     int bx = grid_first(g, 0, r.o.x + s0 * r.d.x, r.y.x), by = grid_first(g, 1, r.o.y + s0 * r.d.y, r.y.y),
         bz = grid_first(g, 2, r.o.z + s0 * r.d.z, r.y.z);
     float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),

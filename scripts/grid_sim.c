@@ -158,7 +158,7 @@ static void build_grid(double cell_target) {
 static uint32_t *fr_off, *fr_list;
 static uint8_t (*fr_s)[6], (*fr_l)[6];
 static int fr_on, start_on;
-static float start_t = 0.0625f;
+static float start_t = 0.09375f;
 static int listed_in(long c, uint32_t k) {
     for (uint32_t q = cell_off[c]; q < cell_off[c + 1]; ++q) if (cell_list[q] == k) return 1;
     return 0;
@@ -166,7 +166,7 @@ static int listed_in(long c, uint32_t k) {
 static void build_faces(void) {
     fr_on = getenv("FACES") != NULL;
     start_on = getenv("START") != NULL;
-    if (start_on) start_t = (float)atof(getenv("START")) > 0.0f ? (float)atof(getenv("START")) : 0.0625f;
+    if (start_on) start_t = (float)atof(getenv("START")) > 0.0f ? (float)atof(getenv("START")) : 0.09375f;
     long total = (long)gn[0] * gn[1] * gn[2];
     int ax0 = 0, ax1 = 2;  /* the plane: two axes with most cells */
     { int o[3] = {0, 1, 2};
@@ -265,7 +265,7 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
     int ic[3], stp[3];
     float tn[3];
     for (int a = 0; a < 3; ++a) {
-        /* the kernel starts the walk in the cell of the ray's point at t = 1/16 (mm_grid.h) */
+        /* the kernel starts the walk in the cell of the ray's point at t = 3/32 (mm_grid.h) */
         const float ps = start_on ? oo[a] + start_t * dd[a] : oo[a];
         int i = (int)floorf((ps - gmin[a]) * ginv[a]);
         if (i < 0) i = 0;
