@@ -738,8 +738,13 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run from block-local rings; built for
     // the grid search and the lean BVH form with records in LDS (other forms run without it)
     // (auto: with the whole search structure in LDS -- the grid image, or BVH nodes + compact records; the N=64
-    // scene's records read through L1/L2 gain nothing from it: C5 frame 231.4 vs 227.7 ms without)
-    const bool defer_on = c->opt_defer > 0 || (c->opt_defer < 0 && (mode == 11 || mode == 3));
+    // scene's records read through L1/L2 gain nothing from it: C5 frame 231.4 vs 227.7 ms without) and paths of
+    // at least 8 bounces (below, the staging + resolve outweigh the tail saved: C2's 4 bounces, 20 frames per
+    // launch, 0.404 vs 0.384 ms/frame; C3's 8: 3.25 vs 3.60 -- profiles/r02_ab_defer_bounces.txt) -- or samples
+    // that are staged anyway (64 % spp != 0: no fused resolve)
+    const bool defer_on =
+        c->opt_defer > 0 ||
+        (c->opt_defer < 0 && (mode == 11 || mode == 3) && (e->bounce_limit >= 8u || 64 % e->spp != 0));
     const bool defer = persist && (defer_on || wave) && wavepersist_defer_built(mode, form) &&
                        (wave || (uint64_t)w * h * e->spp * n_frames >= c->opt_defer_min);
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
