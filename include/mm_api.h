@@ -176,7 +176,8 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_DICT_NODES 20  /* BVH forms 5/7: BVH nodes dictionary-coded (8-bit indices into the scene's
                                   <= 256 distinct bound values, 12 B per node) so the whole tree sits in LDS:
                                   1 when the plain nodes do not fit and no explicit split size is set (default),
-                                  2 always when it fits (tests), 0 off */
+                                  2 always when it fits (tests), 0 off.  Read by mm_upload_scene: with 0 there
+                                  the dictionary is not built (MM_INFO_DICT_OK 0) until the next upload */
 #define MM_OPT_DEFER      21  /* wave-persistent kernel: once at most this many lanes of a wave still trace
                                   (past bounce_limit only mirror-hit paths run on), those paths' states go to
                                   their block's tail ring (512 entries) and the block's waves take 64 of them at

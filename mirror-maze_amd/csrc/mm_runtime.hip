@@ -13,6 +13,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "grid_build.h"
@@ -435,23 +436,27 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
             packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
         }
     // Dictionary-coded nodes (mode 10): the distinct bound values of the
-    // production array, 8-bit indices when there are at most 256
-    std::vector<float> dict;
-    for (const float4& f : packed) {
-        dict.push_back(f.x);
-        dict.push_back(f.y);
-    }
-    for (size_t i = 0; i < packed.size(); i += 2) {
-        dict.push_back(packed[i].z);
-        dict.push_back(packed[i].w);
-    }
+    // production array, 8-bit indices when there are at most 256.  Skipped
+    // with MM_OPT_DICT_NODES 0; the scan stops at the 257th distinct value.
     auto fbits = [](float x) { uint32_t b; std::memcpy(&b, &x, 4); return b; };
-    std::sort(dict.begin(), dict.end(), [&](float a, float b) { return fbits(a) < fbits(b); });
-    dict.erase(std::unique(dict.begin(), dict.end(), [&](float a, float b) { return fbits(a) == fbits(b); }),
-               dict.end());
-    const bool dict_ok = dict.size() <= 256;
+    std::vector<float> dict;
+    bool dict_ok = c->opt_dict != 0;
+    if (dict_ok) {
+        std::unordered_set<uint32_t> seen;
+        auto add = [&](float x) {
+            if (seen.insert(fbits(x)).second) {
+                dict.push_back(x);
+                if (dict.size() > 256) dict_ok = false;
+            }
+        };
+        for (size_t i = 0; i < packed.size() && dict_ok; i += 2) {
+            add(packed[i].x); add(packed[i].y); add(packed[i].z); add(packed[i].w);
+            add(packed[i + 1].x); add(packed[i + 1].y);
+        }
+    }
     std::vector<uint32_t> dict_words;
     if (dict_ok) {
+        std::sort(dict.begin(), dict.end(), [&](float a, float b) { return fbits(a) < fbits(b); });
         auto code = [&](float x) {
             const uint32_t b = fbits(x);
             return (uint32_t)(std::lower_bound(dict.begin(), dict.end(), x,
