@@ -204,10 +204,54 @@ def pmc_profile(args, frames_per_launch, k_avg_s, world):
          "valu_lane_ops_tops": (round(rec["valu_lane_ops_per_launch"] * scale / k_avg_s / 1e12, 3)
                                 if rec.get("valu_lane_ops_per_launch") else None),
          "profile_kernel_avg_ms": rec.get("kernel_avg_ms"),
+         # the record alone: its lane-ops per launch / its own mean launch time / peak
+         "profile_frac": (round(rec["valu_lane_ops_per_launch"] / (rec["kernel_avg_ms"] / 1e3) / 1e12
+                                / VALU_PEAK_TOPS, 4)
+                          if rec.get("valu_lane_ops_per_launch") and rec.get("kernel_avg_ms") else None),
          "note": ("rocprofv3 --pmc passes: HBM = 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE; lane "
                   "utilisation = SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU); issue share = SQ_INSTS_VALU / "
                   "(1024 SIMDs x cycles / 2); per launch, scaled to this run's frames per launch")}
     return m, round(hbm)
+
+
+def roofline(ops, alg_bytes, k_avg_s, k_launches, frames_per_launch, measured, traffic, contexts, kern_res):
+    """The dominant kernel's roofline object.  Headline (achieved / frac): the
+    hardware's executed fp32 VALU lane-ops per launch from the same-source PMC
+    record (SQ_INSTS_VALU x 64 x lane utilisation) / this run's mean launch
+    time, against 78.6 T lane-ops/s.  Without a PMC
+    record of these sources the headline falls back to the reference-walk
+    model and says so in "basis".  The reference-walk VALU model and the
+    136 B/ray HBM model are kept as labelled sub-objects."""
+    ref_tops = ops / k_avg_s / 1e12
+    lane_tops = measured.get("valu_lane_ops_tops") if isinstance(measured, dict) else None
+    hw = lane_tops is not None
+    achieved = lane_tops if hw else ref_tops
+    return {
+        "bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
+        "basis": ("executed fp32 VALU lane-ops (PMC: SQ_INSTS_VALU x 64 x SQ_THREAD_CYCLES_VALU / "
+                  "(64 SQ_ACTIVE_INST_VALU), profiles/pmc_<config>.json of these sources) per launch / mean "
+                  "launch time" if hw else
+                  "reference_equivalent: no PMC record of these sources (see reference_equivalent)"),
+        "peak_basis": "256 CU x 4 SIMD x 32 fp32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md)",
+        "kernel": "k_trace_wavepersist", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
+        "launches": k_launches, "frames_per_launch": round(frames_per_launch, 3),
+        "timing": ("HIP events around each launch on its stream" +
+                   ("; 2 contexts: consecutive launches overlap, so a launch's "
+                    "span includes time shared with its neighbours" if contexts > 1 else "")),
+        "kernel_resources": kern_res,
+        "reference_equivalent": {
+            "achieved": round(ref_tops, 3), "frac": round(ref_tops / VALU_PEAK_TOPS, 4),
+            "ops": ("fp32 VALU lane-ops the reference BVH walk would execute on the timed frames (SURVEY 8d "
+                    "model: 25 per AABB test + 71 per rect test, counted by the BVH loop form) per launch / "
+                    "mean launch time: useful work per second, not what this kernel executes")},
+        "model_hbm": {"bytes_per_ray": BYTES_PER_RAY, "bytes_per_launch": round(alg_bytes),
+                      "achieved_gbs": round(alg_bytes / k_avg_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+                      "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                      "note": ("SURVEY 8(d) accounting model of a SoA wavefront (136 B/ray + 16 "
+                               "B/px), not traffic: the megakernel keeps path state in registers")},
+        "measured": measured,
+    }
 
 
 def main():
@@ -310,6 +354,7 @@ def main():
 
     acc_tile = (torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev)
                 if args.accumulate else None)
+    trace_end = [torch.cuda.Event(enable_timing=True)] if distributed else None
 
     def step(k, frame, stats=False):
         slot = k % active[0]
@@ -318,11 +363,15 @@ def main():
                 _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame, flags=MM_EXT_ACCUMULATE),
                                               0, y0, W, my_rows, y_stride=y_stride, out=acc_tile[:my_rows],
                                               stats=stats)
+                if trace_end is not None:
+                    trace_end[0].record(streams[slot])
                 return st
             tile = gatherer.tile() if gatherer else tiles1[slot]
             ft = ftiles[slot] if rgba8 else tile
             _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
                                           y_stride=y_stride, out=ft[:my_rows], stats=stats)
+            if trace_end is not None:
+                trace_end[0].record(streams[slot])
             if rgba8:
                 rens[slot].quantize(ft[:my_rows], out=tile[:my_rows])
             if gatherer:
@@ -337,6 +386,8 @@ def main():
         with torch.cuda.stream(streams[slot]):
             _, st = rens[slot].trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), n, 0, y0, W, my_rows,
                                                  y_stride=y_stride, out=batch_buf[:n], stats=stats)
+            if trace_end is not None:  # the launch's end on its stream (exposed-gather clock, N > 1)
+                trace_end[0].record(streams[slot])
             if bgather:
                 tl = bgather.tiles(n)
                 for f in range(n):
@@ -447,11 +498,26 @@ def main():
     if acc_tile is not None:
         gather_accumulated()  # C5: one gather of the accumulated frame, inside the timed region
     flush_gathers()  # the last frames' gathers + assembly are inside the timed region
+    assembled = None
+    if distributed:  # the frame is on rank 0 (assembled) / this rank's gather done: exposed-gather clock
+        assembled = torch.cuda.Event(enable_timing=True)
+        assembled.record(asm_stream if rank == 0 else torch.cuda.current_stream(dev))
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     drain()
+    for r in rens:  # errors the timed launches raised on the GPU (naming the call), outside the timing
+        r.sync()
+    exposed_ms = float(trace_end[0].elapsed_time(assembled)) if distributed else None
+    # code-object facts of the timed kernel (hipFuncGetAttributes), before the counting re-runs below
+    from mirror_maze import MM_INFO_LAST_DEFER, MM_INFO_LAST_SCRATCH, MM_INFO_LAST_STATIC_LDS, MM_INFO_LAST_VGPRS
+
+    kern_res = {"vgprs_per_lane": int(rens[0].scene_info(MM_INFO_LAST_VGPRS)),
+                "scratch_bytes_per_lane": int(rens[0].scene_info(MM_INFO_LAST_SCRATCH)),
+                "static_lds_bytes_per_block": int(rens[0].scene_info(MM_INFO_LAST_STATIC_LDS)),
+                "tail_rings": bool(rens[0].scene_info(MM_INFO_LAST_DEFER)),
+                "source": "hipFuncGetAttributes of the timed instance (scripts/kernel_resources.py: spill counts)"}
     k_ms = k_launches = 0
     for r in rens[:active[0]]:
         ms, n = r.kernel_timing(reset=True)
@@ -469,6 +535,8 @@ def main():
         progress(f"counting rays: frame {i + 1}/{args.steps}")
     drain()
     from mirror_maze import MM_INFO_LEAN, MM_TRAV_LEAF_INTERIOR, MM_TRAV_LEAN
+    from mirror_maze import MMError
+
     counter = Renderer(local)
     counter.upload_scene(scene)
     counter.set_option(7, MM_TRAV_LEAN if counter.scene_info(MM_INFO_LEAN) else MM_TRAV_LEAF_INTERIOR)
@@ -476,8 +544,13 @@ def main():
     cnt_out = torch.empty((my_rows, W, 4), dtype=torch.float32, device=dev)
     with torch.cuda.stream(counter.own_stream()):
         for i in range(args.steps):
-            _, st = counter.trace_tile(u, make_ext(spp, bl, ml, frame=i), 0, y0, W, my_rows, y_stride=y_stride,
-                                       out=cnt_out, stats=True)
+            try:
+                _, st = counter.trace_tile(u, make_ext(spp, bl, ml, frame=i), 0, y0, W, my_rows,
+                                           y_stride=y_stride, out=cnt_out, stats=True)
+            except MMError:  # form 7 needs the tree + records in LDS (N=64: form 5, the same counts)
+                counter.set_option(7, MM_TRAV_LEAF_INTERIOR)
+                _, st = counter.trace_tile(u, make_ext(spp, bl, ml, frame=i), 0, y0, W, my_rows,
+                                           y_stride=y_stride, out=cnt_out, stats=True)
             visits += st.node_visits; rtests += st.rect_tests; ref_rays += st.rays
             progress(f"counting reference work: frame {i + 1}/{args.steps}")
     torch.cuda.synchronize(dev)
@@ -485,9 +558,28 @@ def main():
     assert ref_rays == rays or args.accumulate, (ref_rays, rays)
     counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
     t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist_info = None
     if distributed:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
+        # per-rank kernel time and exposed gather (so a SCALE shortfall splits into trace imbalance vs gather)
+        k_lo = torch.tensor([k_ms, exposed_ms], dtype=torch.float64, device=dev)
+        k_hi = k_lo.clone()
+        dist.all_reduce(k_lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(k_hi, op=dist.ReduceOp.MAX)
+        n_gathers = (bgather.launch if bgather else gatherer.k) if (bgather or gatherer) else 0
+        dist_info = {
+            "rccl_world": dist.get_world_size(), "backend": str(dist.get_backend()),
+            "kernel_ms_per_rank": {"rank0": round(k_ms, 3), "min": round(float(k_lo[0]), 3),
+                                   "max": round(float(k_hi[0]), 3)},
+            "exposed_gather_ms": {"rank0": round(exposed_ms, 3), "max": round(float(k_hi[1]), 3),
+                                  "what": ("end of the last timed trace launch -> the frame assembled on rank 0 "
+                                           "(other ranks: their gather done), HIP events on the device; includes "
+                                           "waiting for the slowest rank's launch")},
+            "frames_per_gather": (round(args.steps / max(k_launches, 1), 2) if batch[0] > 1 else 1),
+            "gathers_total": n_gathers,
+            "bytes_per_rank_per_frame": rows_max(H, world) * W * (4 if rgba8 else 16),
+        }
     rays_all, paths_all, visits_all, rtests_all = (float(x) for x in counts.tolist())
     elapsed = float(t_el.item())
 
@@ -532,23 +624,9 @@ def main():
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),
                        "node_visits_per_ray": round(visits_all / max(rays_all, 1), 2),
                        "rect_tests_per_ray": round(rtests_all / max(rays_all, 1), 2)},
-            "roofline": {"bound": "valu", "achieved": round(ops / k_avg_s / 1e12, 3), "peak": VALU_PEAK_TOPS,
-                         "unit": "TFLOP/s", "frac": round(ops / k_avg_s / 1e12 / VALU_PEAK_TOPS, 4),
-                         "traffic": traffic,
-                         "ops": ("fp32 VALU lane-ops of the reference BVH walk on the timed frames (SURVEY 8d "
-                                 "model: 25 per AABB test + 71 per rect test, counted by the BVH loop form) "
-                                 "per launch / mean launch time; peak = 256 CU x 128 lanes/clk x 2.4 GHz"),
-                         "kernel": "k_trace_wavepersist", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
-                         "launches": k_launches, "frames_per_launch": round(frames_per_launch, 3),
-                         "timing": ("HIP events around each launch on its stream" +
-                                    ("; 2 contexts: consecutive launches overlap, so a launch's "
-                                     "span includes time shared with its neighbours" if active[0] > 1 else "")),
-                         "model_hbm": {"bytes_per_ray": BYTES_PER_RAY, "bytes_per_launch": round(alg_bytes),
-                                       "achieved_gbs": round(alg_bytes / k_avg_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
-                                       "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                                       "note": ("SURVEY 8(d) accounting model of a SoA wavefront (136 B/ray + 16 "
-                                                "B/px), not traffic: the megakernel keeps path state in registers")},
-                         "measured": measured},
+            "roofline": roofline(ops, alg_bytes, k_avg_s, k_launches, frames_per_launch, measured, traffic,
+                                 active[0], kern_res),
+            "distributed": dist_info,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -126,7 +126,10 @@ int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
  * work queue, so the ~0.4 ms tail in which the last waves finish their last
  * chunks is paid once per launch instead of once per frame (throughput mode
  * for frame sequences; a frame's result is only complete when the launch is).
- * Needs the wave-persistent kernel with the fused resolve (64 % spp == 0);
+ * Needs the wave-persistent kernel with the fused resolve (64 % spp == 0) or
+ * with the mirror-tail deferral (any spp: samples staged per frame and
+ * resolved in one pass, at most 2^29 staged paths = 8 GiB per launch; over
+ * that a fusable launch runs without deferral, others get MM_ERR_INVALID);
  * MM_EXT_ACCUMULATE is rejected (frames of one launch run concurrently). */
 int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext, uint32_t n_frames,
                           uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
@@ -193,6 +196,15 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   default 2^24: below it the staged resolve outweighs the tail saved -- C1
                                   0.039 vs 0.033 ms/frame, C2 x 5 frames 0.49 vs 0.42; 10 frames of rank 0 of an
                                   8-way C3 split, 20.7 M paths, 0.50 vs 0.51); 0: always */
+#define MM_OPT_FAULT_INJECT 23 /* tests of the error path (results are then invalid): 0 off (default); 1 every
+                                  wave-persistent launch raises an injected fault (error bit 3); 2 the tail
+                                  rings' protocol waits give up at once (bit 2 when a wait was needed; the
+                                  samples whose ring entries were skipped are NaN) */
+/* Default builds hold the kernels MM_PIPE_AUTO can select; values that need
+ * the A/B-only variants (MM_OPT_PERSIST 0, MM_OPT_TRAVERSAL 0,
+ * MM_OPT_LDS_SPLIT > 1, MM_OPT_DICT_NODES 2, BVH form 7 without nodes +
+ * records in LDS) return MM_ERR_UNSUPPORTED unless the library was built with
+ * `make EXTRA=-DMM_AB_VARIANTS` (mm_version() then ends in "+ab"). */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Facts about the uploaded scene's search structures (double-valued):
@@ -206,7 +218,11 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
  *   MM_INFO_DICT_OK          1 if the nodes have <= 256 distinct bound values (dictionary nodes possible)
  *   MM_INFO_LAST_FORM        query method of the last wave-persistent launch (MM_OPT_TRAVERSAL value)
  *   MM_INFO_LAST_LDS_MODE    its LDS mode (trace_kernels.hip: 0, 1, 3, 6, 7, 10 BVH; 11-13 grid)
- *   MM_INFO_GRID_FACES       1 if the grid cells carry per-face list ranges (64-bit cell words) */
+ *   MM_INFO_GRID_FACES       1 if the grid cells carry per-face list ranges (64-bit cell words)
+ *   MM_INFO_LAST_DEFER       1 if the last mm_trace_tile* call ran the mirror-tail rings
+ *   MM_INFO_LAST_VGPRS       VGPRs per lane of the last wave-persistent kernel (code-object metadata)
+ *   MM_INFO_LAST_SCRATCH     its private (scratch) bytes per lane: VGPR spills + traversal stack
+ *   MM_INFO_LAST_STATIC_LDS  its static LDS bytes per block (the tail ring's words) */
 #define MM_INFO_GRID_OK          1
 #define MM_INFO_GRID_CELLS_X     2
 #define MM_INFO_GRID_CELLS_Y     3
@@ -220,6 +236,10 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
 #define MM_INFO_LAST_FORM        11
 #define MM_INFO_LAST_LDS_MODE    12
 #define MM_INFO_GRID_FACES       13
+#define MM_INFO_LAST_DEFER       14
+#define MM_INFO_LAST_VGPRS       15
+#define MM_INFO_LAST_SCRATCH     16
+#define MM_INFO_LAST_STATIC_LDS  17
 int  mm_scene_info(const mm_ctx* ctx, int key, double* value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64
@@ -228,8 +248,24 @@ int  mm_scene_info(const mm_ctx* ctx, int key, double* value);
  * chunks it traced.  NULL turns it off (default).  scripts/timeline_probe.py */
 int  mm_set_wave_timeline(mm_ctx* ctx, unsigned long long* dev_buf, uint32_t n_waves);
 
-/* Wait for all work queued by this context. */
+/* Wait for all work queued by this context; returns the error of the oldest
+ * mm_trace_tile* call that failed on the GPU and was not reported yet. */
 int  mm_sync(mm_ctx* ctx);
+
+/* Asynchronous errors.  mm_trace_tile / mm_trace_tile_frames return before
+ * the GPU runs them; each such call is numbered (1, 2, ...) and its launches
+ * publish their error flags (traversal stack overflow, a tail-ring protocol
+ * timeout, an injected fault) into host-mapped status words when they end.
+ * A call that failed is reported -- its return code, and mm_last_error naming
+ * "call #N (what it traced)" -- by the first of: the next mm_trace_tile* call
+ * on the context (which is then not enqueued), mm_sync, or mm_call_status(N).
+ * It is never attributed to a later call's own work.  (The reference has no
+ * error path: a Metal command buffer fails silently, src/main.rs:893-894.) */
+#define MM_PENDING 1
+int  mm_last_call(const mm_ctx* ctx, uint64_t* call_id);
+/* Without waiting: MM_OK (finished clean), MM_PENDING (still running) or the
+ * call's error code (message in mm_last_error). */
+int  mm_call_status(mm_ctx* ctx, uint64_t call_id);
 
 /* Per-kernel timing of the dominant (ray-trace) kernel: when enabled, every
  * trace-kernel launch is bracketed by HIP events on the context's stream.

@@ -60,7 +60,27 @@ struct TileJob {
     // defer_from >= 2^30: off.
     uint32_t defer_from = 1u << 30, defer_lanes = 0;
     TailQueue tail;
+    // Per-launch status word (host-mapped pinned memory, mm_runtime.hip): the
+    // last wave of the launch moves the error flag into it, | kStatusDone, so
+    // the host attributes an error to the call that launched it without a
+    // sync.  Null: the error flag stays sticky (parity mode reads it itself).
+    uint32_t* status = nullptr;
+    // Polls a tail-ring protocol wait may take before it gives up (error bit
+    // 2); the drain's wait for block-mates is bounded by lack of progress
+    // instead (trace_kernels.hip).  MM_OPT_FAULT_INJECT 2 sets 0.
+    uint32_t ring_spin = 1u << 21;
+    // MM_OPT_FAULT_INJECT 1: the launch raises error bit 3 (tests of the
+    // error path).
+    uint32_t fault = 0;
 };
+
+// Error flag bits (aux word 4, and the status word's low bits).
+constexpr uint32_t kErrStack = 1u, kErrRing = 2u, kErrInjected = 8u;
+constexpr uint32_t kStatusDone = 0x80000000u;
+
+// One-thread kernel that publishes a non-persistent launch's error flag into
+// its status word (the persistent kernel's last wave does this itself).
+hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s);
 
 struct MegaOpts {
     bool reference = false;   // traverse_reference (IEEE division), A/B baseline
@@ -83,8 +103,14 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s);
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
-// Whether the tail-deferral variant exists for this (LDS mode, form).
+// Whether the tail-deferral variant / any variant exists for this (LDS mode, form).
 bool wavepersist_defer_built(int lds_mode, int form);
+bool wavepersist_built(int lds_mode, int form);
+// Register / scratch / LDS use of the (kStats = false) instance.
+hipError_t wavepersist_attributes(int lds_mode, int form, bool defer, hipFuncAttributes* a);
+// Built with -DMM_AB_VARIANTS (the A/B-only placements and k_trace_mega's
+// non-reference forms).
+bool ab_variants_built();
 // Display stage (display.hip).
 hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H, hipStream_t s);
 hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,

@@ -8,11 +8,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -98,7 +101,32 @@ struct mm_ctx {
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
     size_t prof_used = 0;              // events recorded since last reset
+    // Per-launch status words (host-mapped pinned memory): launch L of the
+    // context writes slot L % kStatusSlots when it ends (error bits |
+    // kStatusDone).  Each mm_trace_tile* call is a numbered "call" owning a
+    // run of launches; a call whose launches raised an error is reported,
+    // naming the call, by the next call on the context, mm_sync or
+    // mm_call_status -- never blamed on a later call's work.
+    uint32_t* h_status = nullptr;
+    uint32_t* d_status = nullptr;
+    std::vector<uint64_t> slot_owner;  // launch id + 1 holding each slot, 0 = free
+    uint64_t launch_seq = 0, call_seq = 0;
+    struct Call { uint64_t id, first, n; std::string what; uint32_t bits; };
+    struct Failed { uint64_t id; uint32_t bits; std::string what; bool reported; };
+    std::deque<Call> pending;
+    std::deque<Failed> failed;  // the last kFailedKept failed calls
+    int opt_fault = 0;           // MM_OPT_FAULT_INJECT
+    bool last_defer = false;     // the last trace call ran the tail rings
+    int last_kern_mode = -1, last_kern_form = -1;  // for MM_INFO_LAST_VGPRS / _SCRATCH
+    bool last_kern_defer = false;
 };
+
+constexpr uint32_t kStatusSlots = 1024;
+constexpr size_t kFailedKept = 64;
+// Staged samples (tail deferral / no fused resolve) per launch: whole rows up
+// to this many paths (16 B each: 8 GiB).  A multi-frame launch over the cap
+// runs without deferral (fused resolve) or is refused.
+constexpr uint64_t kStagePathsMax = 1ull << 29;
 
 namespace {
 
@@ -246,11 +274,85 @@ int read_aux(mm_ctx* c, mm_stats* st) {
     return MM_OK;
 }
 
+// ---- per-call status (see mm_ctx::h_status) -------------------------------
+uint32_t status_load(const mm_ctx* c, uint64_t launch) {
+    return __atomic_load_n(c->h_status + launch % kStatusSlots, __ATOMIC_ACQUIRE);
+}
+
+// Device address of the status word for the next launch.  A slot still held
+// by a launch kStatusSlots earlier that has not finished is waited for.
+int next_status(mm_ctx* c, uint32_t*& dev_word) {
+    const uint64_t id = c->launch_seq;
+    const uint32_t s = (uint32_t)(id % kStatusSlots);
+    if (c->slot_owner[s] && !(status_load(c, c->slot_owner[s] - 1) & kStatusDone)) {
+        HIPC(c, hipStreamSynchronize(c->stream));
+        if (!(status_load(c, c->slot_owner[s] - 1) & kStatusDone)) HIPC(c, hipDeviceSynchronize());
+        if (!(status_load(c, c->slot_owner[s] - 1) & kStatusDone))
+            return fail(c, MM_ERR_HIP, "status word of an earlier launch never completed");
+    }
+    if (c->slot_owner[s]) {  // fold the finished occupant's bits into its call, if still pending
+        const uint64_t prev = c->slot_owner[s] - 1;
+        for (auto& k : c->pending)
+            if (prev >= k.first && prev < k.first + k.n) k.bits |= status_load(c, prev) & ~kStatusDone;
+    }
+    __atomic_store_n(c->h_status + s, 0u, __ATOMIC_RELEASE);
+    c->slot_owner[s] = id + 1;
+    c->launch_seq = id + 1;
+    dev_word = c->d_status + s;
+    return MM_OK;
+}
+
+std::string error_text(uint32_t bits) {
+    std::string s;
+    auto add = [&](const char* m) { s += s.empty() ? m : std::string("; ") + m; };
+    if (bits & kErrStack) add("traversal stack overflow (depth > 50)");
+    if (bits & kErrRing) add("tail ring wait timed out (kernel protocol error)");
+    if (bits & kErrInjected) add("injected fault (MM_OPT_FAULT_INJECT)");
+    return s.empty() ? "unknown error" : s;
+}
+int error_code(uint32_t bits) { return (bits & ~kErrStack) ? MM_ERR_HIP : MM_ERR_STACK; }
+
+// Fold finished calls' status words into the failed list (non-blocking).
+void poll_calls(mm_ctx* c) {
+    for (auto it = c->pending.begin(); it != c->pending.end();) {
+        uint32_t bits = it->bits;
+        bool done = true;
+        for (uint64_t l = it->first; l < it->first + it->n && done; ++l) {
+            // a slot reused by a later launch: this launch finished, its bits are in it->bits
+            if (c->slot_owner[l % kStatusSlots] != l + 1) continue;
+            const uint32_t w = status_load(c, l);
+            done = (w & kStatusDone) != 0;
+            bits |= w & ~kStatusDone;
+        }
+        if (!done) { ++it; continue; }
+        if (bits) {
+            c->failed.push_back({it->id, bits, it->what, false});
+            if (c->failed.size() > kFailedKept) c->failed.pop_front();
+        }
+        it = c->pending.erase(it);
+    }
+}
+
+// The oldest unreported failed call, as this call's return code.
+int report_failure(mm_ctx* c, const char* suffix) {
+    poll_calls(c);
+    for (auto& f : c->failed)
+        if (!f.reported) {
+            f.reported = true;
+            return fail(c, error_code(f.bits),
+                        "call #" + std::to_string(f.id) + " (" + f.what + ") failed on the GPU: " +
+                            error_text(f.bits) + suffix);
+        }
+    return MM_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-const char* mm_version(void) { return "mirror-maze-amd 0.1 gfx950"; }
+const char* mm_version(void) {
+    return ab_variants_built() ? "mirror-maze-amd 0.3 gfx950+ab" : "mirror-maze-amd 0.3 gfx950";
+}
 
 int mm_create(int device, mm_ctx** out) {
     if (!out) return MM_ERR_INVALID;
@@ -271,6 +373,15 @@ int mm_create(int device, mm_ctx** out) {
     if (rc == MM_OK) chk(hipEventCreate(&c->ev1), "hipEventCreate");
     if (rc == MM_OK) chk(hipMalloc((void**)&c->d_aux, 8 * sizeof(unsigned long long)), "hipMalloc(aux)");
     if (rc == MM_OK) chk(hipMemset(c->d_aux, 0, 8 * sizeof(unsigned long long)), "hipMemset(aux)");
+    if (rc == MM_OK)
+        chk(hipHostMalloc((void**)&c->h_status, kStatusSlots * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc(status)");
+    if (rc == MM_OK) chk(hipHostGetDevicePointer((void**)&c->d_status, c->h_status, 0), "hipHostGetDevicePointer");
+    if (rc == MM_OK) {
+        std::memset(c->h_status, 0, kStatusSlots * sizeof(uint32_t));
+        c->slot_owner.assign(kStatusSlots, 0);
+    }
     if (rc != MM_OK) {
         fprintf(stderr, "mm_create: %s\n", c->err.c_str());
         mm_destroy(c);
@@ -289,6 +400,7 @@ void mm_destroy(mm_ctx* c) {
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_tail);
+    if (c->h_status) (void)hipHostFree(c->h_status);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -324,6 +436,9 @@ int mm_set_pipeline(mm_ctx* c, int pipe) {
     return MM_OK;
 }
 
+static const char* const kAbOnly =
+    "this A/B-only kernel variant is built only with `make EXTRA=-DMM_AB_VARIANTS` (DESIGN.md §4)";
+
 int mm_set_option(mm_ctx* c, int key, int value) {
     if (!c) return MM_ERR_INVALID;
     switch (key) {
@@ -334,16 +449,19 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_PERSIST:
             if (value != 0 && value != 2) return fail(c, MM_ERR_INVALID, "persist must be 0 or 2");
+            if (value == 0 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
             c->opt_persist = value;
             return MM_OK;
         case MM_OPT_TRAVERSAL:
             if (value != -1 && value != 0 && value != 5 && value != 7 && value != 11)
                 return fail(c, MM_ERR_INVALID, "traversal must be -1 (auto), 0, 5, 7 or 11 (grid search)");
+            if (value == 0 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
         case MM_OPT_LDS_SPLIT:
             if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
+            if (value > 1 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
             c->opt_lds_split = (uint32_t)value;
             return MM_OK;
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
@@ -361,7 +479,12 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_DICT_NODES:
             if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
+            if (value == 2 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
             c->opt_dict = (uint32_t)value;
+            return MM_OK;
+        case MM_OPT_FAULT_INJECT:
+            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "fault inject must be 0, 1 or 2");
+            c->opt_fault = value;
             return MM_OK;
         default: return fail(c, MM_ERR_INVALID, "unknown option");
     }
@@ -385,6 +508,18 @@ int mm_scene_info(const mm_ctx* c, int key, double* value) {
         case MM_INFO_LAST_FORM: *value = c->last_form; return MM_OK;
         case MM_INFO_LAST_LDS_MODE: *value = c->last_mode; return MM_OK;
         case MM_INFO_GRID_FACES: *value = c->grid_ok && c->grid_wide ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_LAST_DEFER: *value = c->last_defer ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_LAST_VGPRS:
+        case MM_INFO_LAST_SCRATCH:
+        case MM_INFO_LAST_STATIC_LDS: {
+            if (c->last_kern_mode < 0) return MM_ERR_INVALID;
+            hipFuncAttributes a{};
+            if (wavepersist_attributes(c->last_kern_mode, c->last_kern_form, c->last_kern_defer, &a) != hipSuccess)
+                return MM_ERR_HIP;
+            *value = key == MM_INFO_LAST_VGPRS ? a.numRegs
+                     : key == MM_INFO_LAST_SCRATCH ? (double)a.localSizeBytes : (double)a.sharedSizeBytes;
+            return MM_OK;
+        }
         default: return MM_ERR_INVALID;
     }
 }
@@ -684,6 +819,19 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
     const size_t recs_b = 40 * (size_t)c->n_rects;
     const size_t dict_b = 256 * sizeof(float) + 12 * (size_t)c->n_nodes;
     const bool dict_fits = c->opt_dict && c->dict_ok && dict_b <= budget;
+    if (!ab_variants_built()) {
+        // default build: nodes + records in LDS (lean form 7 or form 5), nodes only (form 5), or nothing
+        if (c->opt_lds && c->opt_lds_rects && nodes_b + recs_b <= budget) {
+            mode = 3;
+        } else {
+            if (form == kFormLean && !auto_form)
+                return fail(c, MM_ERR_UNSUPPORTED,
+                            std::string("loop form 7 without nodes + records in LDS: ") + kAbOnly);
+            form = kFormLeafInterior;
+            mode = (c->opt_lds && nodes_b <= budget) ? 1 : 0;
+        }
+        return MM_OK;
+    }
     if (!c->opt_lds) {
         mode = 0;
     } else if (c->opt_dict == 2 && dict_fits) {
@@ -713,6 +861,8 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
 int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_frames, uint32_t x0, uint32_t y0,
                     uint32_t w, uint32_t h, uint32_t y_stride, float* out_dev, mm_stats* stats) {
     if (!c) return MM_ERR_INVALID;
+    // an earlier call that failed on the GPU is reported first, by name; this call is then not enqueued
+    if (int rc0 = report_failure(c, "; this call was not enqueued")) return rc0;
     if (!c->has_scene) return fail(c, MM_ERR_NO_SCENE, "mm_trace_tile: no scene uploaded");
     if (!u || !e || !out_dev) return fail(c, MM_ERR_INVALID, "mm_trace_tile: null argument");
     if (!(u->view_w >= 1.0f && u->view_w <= 65536.0f && u->view_h >= 1.0f && u->view_h <= 65536.0f))
@@ -725,15 +875,15 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: bounce or mirror limit above 32767");
     if ((uint64_t)x0 + w > W || (uint64_t)y0 + (uint64_t)(h - 1) * y_stride >= H)
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: tile outside the frame");
+    if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
     HIPC(c, hipSetDevice(c->device));
     const bool want_stats = (e->flags & MM_EXT_COUNT_STATS) != 0;
-    // Bound the per-sample staging buffer: process whole rows, <= 64 Mi paths
-    // (32 Mi in the wavefront pipeline).  With the fused resolve there is no
-    // staging buffer: one launch covers up to 2^31 paths (a whole C5 frame).
     const uint64_t row_paths = (uint64_t)w * e->spp;
+    const uint64_t tile_paths = row_paths * h;
     // MM_PIPE_WAVEFRONT: the wave-persistent kernel with mirror-tail deferral (compaction) always on
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
     const bool persist = c->pipe != MM_PIPE_REFERENCE && (wave || c->opt_persist == 2);
+    if (!persist && c->pipe != MM_PIPE_REFERENCE && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
     int form = 0, mode = 0;
     DevScene sc = dev_scene(c);
     if (persist) {
@@ -750,14 +900,30 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     const bool defer_on =
         c->opt_defer > 0 ||
         (c->opt_defer < 0 && (mode == 11 || mode == 3) && (e->bounce_limit >= 8u || 64 % e->spp != 0));
-    const bool defer = persist && (defer_on || wave) && wavepersist_defer_built(mode, form) &&
-                       (wave || (uint64_t)w * h * e->spp * n_frames >= c->opt_defer_min);
+    const bool defer_built = persist && wavepersist_defer_built(mode, form);
+    if (wave && !defer_built)
+        return fail(c, MM_ERR_UNSUPPORTED, "MM_PIPE_WAVEFRONT: no tail-deferral kernel for this scene's query "
+                                           "method / LDS placement (grid search, or BVH form 7 with nodes + "
+                                           "records in LDS)");
+    bool defer = defer_built && (defer_on || wave) && (wave || tile_paths * n_frames >= c->opt_defer_min);
+    // the tail ring's static LDS must leave two 1024-thread blocks per CU: a grid image within
+    // 2064 B of the 80 KB budget runs without the rings
+    if (defer && wavepersist_lds_bytes(sc, mode) + (4 + kTailRing) * sizeof(uint32_t) > 80 * 1024) {
+        if (wave) return fail(c, MM_ERR_UNSUPPORTED, "MM_PIPE_WAVEFRONT: grid image + tail ring exceed the LDS budget");
+        defer = false;
+    }
+    const bool fusable = persist && c->opt_fuse && 64 % e->spp == 0;
+    // staging bound: a multi-frame launch stages all its frames at once; past kStagePathsMax it runs without
+    // the rings (fused resolve) if it can
+    if (defer && n_frames > 1 && tile_paths * n_frames > kStagePathsMax && fusable && !wave) defer = false;
     // wave-persistent kernel with whole pixels per 64-path chunk: resolve fused
-    const bool fuse = persist && !defer && c->opt_fuse && 64 % e->spp == 0;
-    const uint64_t batch_paths = (fuse || defer) ? (1ull << 31) : (64ull << 20);
+    const bool fuse = fusable && !defer;
+    // Rows per launch: the fused resolve needs no staging (one launch covers up to 2^31 paths, a whole C5
+    // frame); staged samples (tail deferral, or no fused resolve) are bounded by kStagePathsMax per launch
+    // (64 Mi paths without deferral, where the non-persistent kernels' short launches lose nothing)
+    const uint64_t batch_paths = fuse ? (1ull << 31) : defer ? kStagePathsMax : (64ull << 20);
     const uint32_t rows_per_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(h, batch_paths / row_paths));
     if (row_paths * rows_per_batch > 0xFFFFFFFFull) return fail(c, MM_ERR_INVALID, "mm_trace_tile: row too large");
-    if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
     if (n_frames > 1) {
         // several frames in one launch: the wave-persistent kernel's queue, with the fused resolve or
         // (tail deferral) samples staged per frame
@@ -767,21 +933,26 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         if (e->flags & MM_EXT_ACCUMULATE)
             return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: frames of one launch cannot accumulate into "
                                            "one image");
-        const uint64_t queue = ((row_paths * h + 63) / 64) * 64 * n_frames;
-        if (rows_per_batch < h || queue + (1ull << 24) > 0xFFFFFFFFull)
+        const uint64_t queue = ((tile_paths + 63) / 64) * 64 * n_frames;
+        if (queue + (1ull << 24) > 0xFFFFFFFFull)
             return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: more paths than one launch holds (2^32)");
+        if (defer && tile_paths * n_frames > kStagePathsMax)
+            return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: the frames' staged samples exceed 8 GiB "
+                                           "(2^29 paths) per launch; use fewer frames per launch");
+        if (rows_per_batch < h) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: tile too large for one launch");
     }
     int rc = fuse ? MM_OK : ensure(c, c->d_samples, c->samples_cap,
                                    (size_t)(row_paths * rows_per_batch) * (defer ? n_frames : 1));
     if (rc) return rc;
     TailQueue tq;
     if (defer && (rc = tail_queue(c, tq))) return rc;
-    // aux: [0..3] stats (zeroed only when counted), [4] sticky error flag
-    // (cleared by read_aux), [5] lane-refill counter (zeroed by its launcher),
-    // [6] wave-persistent counter pair (self-cleaning).  No fill kernel on the
-    // default path: see k_trace_wavepersist.
+    // aux: [0..3] stats (zeroed only when counted), [4] error flag (moved into the launch's status word by
+    // the launch itself), [5] lane-refill counter (zeroed by its launcher), [6] wave-persistent counter pair
+    // (self-cleaning).  No fill kernel on the default path: see k_trace_wavepersist.
     if (want_stats) HIPC(c, hipMemsetAsync(c->d_aux, 0, 4 * sizeof(unsigned long long), c->stream));
     if ((rc = begin_timing(c))) return rc;
+    uint32_t* err_dev = reinterpret_cast<uint32_t*>(c->d_aux + 4);
+    const uint64_t call_id = ++c->call_seq, first_launch = c->launch_seq;
     uint32_t launches = 0;
     for (uint32_t j0 = 0; j0 < h; j0 += rows_per_batch) {
         TileJob job;
@@ -799,18 +970,23 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
         job.reserve_cus = c->opt_reserve_cus;
+        job.fault = c->opt_fault == 1 ? 1u : 0u;
+        if (c->opt_fault == 2) job.ring_spin = 0;
         if (defer) {
             job.defer_from = 1;
             job.defer_lanes = c->opt_defer > 0 ? (uint32_t)c->opt_defer : 32u;
             job.tail = tq;
         }
+        if ((rc = next_status(c, job.status))) return rc;
         if ((rc = prof_mark(c))) return rc;
         const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
         if (persist) {
             c->last_form = form >= kFormGrid ? kFormGrid : form;
             c->last_mode = mode;
-            HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux,
-                                             reinterpret_cast<uint32_t*>(c->d_aux + 4),
+            c->last_kern_mode = mode;
+            c->last_kern_form = form;
+            c->last_kern_defer = defer;
+            HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux, err_dev,
                                              reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
                                              c->stream));
         } else {
@@ -818,10 +994,10 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             mo.reference = c->pipe == MM_PIPE_REFERENCE;
             mo.lds_nodes = lds_fits;
             mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
-            HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux,
-                                      reinterpret_cast<uint32_t*>(c->d_aux + 4), want_stats, mo, c->stream));
+            HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux, err_dev, want_stats, mo, c->stream));
         }
         if ((rc = prof_mark(c))) return rc;
+        if (!persist) HIPC(c, launch_publish_status(err_dev, job.status, c->stream));
         if (fuse) {
             launches += 1;
             continue;
@@ -833,8 +1009,19 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         HIPC(c, launch_resolve(rj, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
         launches += 2;
     }
+    c->last_defer = defer;
+    {
+        char what[160];
+        snprintf(what, sizeof(what), "%s, frames %u..%u, tile (%u, %u) %ux%u / %u, %u spp", n_frames > 1 ?
+                 "mm_trace_tile_frames" : "mm_trace_tile", e->frame, e->frame + n_frames - 1, x0, y0, w, h,
+                 y_stride, e->spp);
+        c->pending.push_back({call_id, first_launch, c->launch_seq - first_launch, what, 0u});
+    }
     if ((rc = end_timing(c, launches))) return rc;
-    if (want_stats) return read_aux(c, stats);
+    if (want_stats) {
+        if ((rc = read_aux(c, stats))) return rc;
+        return report_failure(c, "");  // (synced: this call's own error, if any)
+    }
     return MM_OK;
 }
 
@@ -854,7 +1041,29 @@ int mm_sync(mm_ctx* c) {
     if (!c) return MM_ERR_INVALID;
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
-    return read_aux(c, nullptr);
+    if (int rc = read_aux(c, nullptr)) return rc;
+    return report_failure(c, "");
+}
+
+int mm_last_call(const mm_ctx* c, uint64_t* call_id) {
+    if (!c || !call_id) return MM_ERR_INVALID;
+    *call_id = c->call_seq;
+    return MM_OK;
+}
+
+int mm_call_status(mm_ctx* c, uint64_t call_id) {
+    if (!c) return MM_ERR_INVALID;
+    if (call_id == 0 || call_id > c->call_seq) return fail(c, MM_ERR_INVALID, "mm_call_status: no such call");
+    poll_calls(c);
+    for (const auto& k : c->pending)
+        if (k.id == call_id) return MM_PENDING;
+    for (auto& f : c->failed)
+        if (f.id == call_id) {
+            f.reported = true;
+            return fail(c, error_code(f.bits), "call #" + std::to_string(f.id) + " (" + f.what +
+                                                   ") failed on the GPU: " + error_text(f.bits));
+        }
+    return MM_OK;  // finished clean (or failed so long ago that it is no longer kept)
 }
 
 int mm_set_profiling(mm_ctx* c, int enable) {

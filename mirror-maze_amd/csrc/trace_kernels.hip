@@ -194,8 +194,8 @@ __device__ __forceinline__ F3 path_value(const PathState& p) {
 // block, payload in the queue's records blockIdx.x * kTailRing + slot.  LDS
 // words (static, at constant addresses -- every word of the ring's state that
 // lives in an SGPR across the bounce loop pushes a grid-search value into a
-// spill): ctl[0] = entries reserved, ctl[1] = entries claimed, ctl[2] = waves
-// past the global queue, then one turn word per slot.  Entry n lives in slot
+// spill): ctl[0] = entries reserved, ctl[1] = entries claimed, ctl[2..3]
+// unused, then one turn word per slot.  Entry n lives in slot
 // n % kTailRing; its writer waits for turn == 2 * lap (the previous lap's
 // reader is done), writes the payload, sets 2 * lap + 1; its reader waits for
 // that, loads, sets 2 * lap + 2.  A writer reserves only entries whose
@@ -259,14 +259,25 @@ __device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
     return k;
 }
 
-// Every wait is bounded (~0.1 s): a protocol bug ends the launch with error
-// bit 2 set rather than a grid that never drains.
-constexpr uint32_t kRingSpin = 1u << 21;
-__device__ __forceinline__ void ring_wait(uint32_t* turn, uint32_t want, uint32_t* err) {
+// A protocol wait -- a reader for the writer of its entry, a writer for the
+// previous lap's reader -- waits on a step already under way, so it is
+// bounded (job.ring_spin polls, ~0.1 s): a protocol bug ends the launch with
+// error bit 2 rather than a grid that never drains.  Returns false on timeout;
+// the caller then skips its load / store and poisons the sample slot it
+// knows (NaN), so the failure shows in the output as well as in the flag.
+__device__ __forceinline__ bool ring_wait(uint32_t* turn, uint32_t want, uint32_t* err, uint32_t spin) {
     for (uint32_t i = 0; lds_ld(turn) != want; ++i) {
-        if (i == kRingSpin) { atomicOr(err, 2u); return; }
+        if (i >= spin) {
+            atomicOr(err, kErrRing);
+            return false;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
+    return true;
+}
+
+__device__ __forceinline__ void poison(float4* samples, uint32_t slot, uint32_t n_slots) {
+    if (slot < n_slots) samples[slot] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.0f);
 }
 
 template <bool kStats, typename Q>
@@ -307,7 +318,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             p.mh = 0;
             bool overflow = false;
             bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow);
-            if (overflow) atomicOr(err, 1u);
+            if (overflow) atomicOr(err, kErrStack);
             s = path_value(p);
             if (!job.fuse) samples[fr * n_paths + path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
@@ -337,10 +348,14 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
 // With tail deferral (kDefer): a wave's next chunk is 64 queued
 // tails from its block's ring when there are that many, else 64 new paths
 // from the global queue; once that is out, whatever the ring still holds
-// (deferral off, so the block drains), until every wave of the block is past
-// the global queue and every entry is claimed.  A tail chunk runs the same
-// bounce loop as a new one (and may defer again) -- one copy of the loop in
-// the kernel.
+// (deferral off), and the wave exits as soon as its block's ring is empty.
+// No wave waits for its block-mates: a wave defers tails only before it has
+// seen the global queue out, and after it has seen that it claims from the
+// ring until the ring is empty -- so every tail is claimed by the wave that
+// parked it if by no other (a drain wait for block-mates' last chunks, which
+// last up to bounce_limit + mirror_limit iterations, would need a bound that a
+// valid 32767-bounce chunk outlasts).  A tail chunk runs the same bounce loop
+// as a new one (and may defer again) -- one copy of the loop in the kernel.
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, const Q& q, const TileJob& job,
                                               float4* __restrict__ samples, unsigned long long* stats, uint32_t* err,
@@ -352,11 +367,12 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
     const uint32_t lane = threadIdx.x & 63u;
     const F3 ori = F3{job.u.cam.center[0], job.u.cam.center[1], job.u.cam.center[2]};
     const TailQueue& tq = job.tail;
+    const uint32_t n_slots = n_paths * job.n_frames;
     Counters c;
     ScratchStack stack;
-    uint32_t paths = 0, chunks = 0, idle = 0;
+    uint32_t paths = 0, chunks = 0;
     int defer_from = (int)job.defer_from;  // 2^30 (off) once the global queue is out
-#ifdef MM_RING_CLOCKS  // diagnostics: per wave (main chunks, tail chunks, ring waits, drain idle) wall clock
+#ifdef MM_RING_CLOCKS  // diagnostics: per wave (main chunks, tail chunks, claim retries) wall clock
     uint64_t rc_main = 0, rc_tail = 0, rc_idle = 0;
     uint64_t rc_t0 = 0;
 #endif
@@ -369,15 +385,13 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
         k = __builtin_amdgcn_readfirstlane(k);
         if (!k) {
             if (defer_from == (1 << 30)) {
-                uint32_t done = 0;
-                if (lane == 0)
-                    done = lds_ld(ring_ctl() + 2) == (blockDim.x >> 6) && lds_ld(ring_ctl() + 0) == lds_ld(ring_ctl() + 1);
-                if (__builtin_amdgcn_readfirstlane(done)) break;
-                if (++idle == kRingSpin) {
-                    if (lane == 0) atomicOr(err, 2u);
-                    break;
+                // the claim failed: the ring is empty (exit) or a block-mate's claim won the race (retry)
+                uint32_t left = 0;
+                if (lane == 0) {
+                    const uint32_t claimed = lds_ld(ring_ctl() + 1);
+                    left = lds_ld(ring_ctl() + 0) - claimed;  // (read after claimed)
                 }
-                __builtin_amdgcn_s_sleep(2);
+                if (!__builtin_amdgcn_readfirstlane(left)) break;
 #ifdef MM_RING_CLOCKS
                 rc_idle += wall_clock64() - rc_t0;
 #endif
@@ -385,8 +399,6 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             }
             if (lane == 0) b = atomicAdd(work, 64u);
             if (__builtin_amdgcn_readfirstlane(b) >= n_queue) {
-                if (lane == 0)
-                    __hip_atomic_fetch_add(ring_ctl() + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 defer_from = 1 << 30;
                 continue;
             }
@@ -400,10 +412,15 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             if (live) {
                 const uint32_t seq = __builtin_amdgcn_readfirstlane(first) + lane;
                 const uint32_t lap = ring_lap(seq);
-                ring_wait(ring_turn(seq), 2u * lap + 1u, err);
-                slot = tail_load(tq, blockIdx.x * kTailRing + seq % kTailRing, p);
-                // (the release waits for the loads above)
-                __hip_atomic_store(ring_turn(seq), 2u * lap + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t rec = blockIdx.x * kTailRing + seq % kTailRing;
+                if (ring_wait(ring_turn(seq), 2u * lap + 1u, err, job.ring_spin)) {
+                    slot = tail_load(tq, rec, p);
+                    // (the release waits for the loads above)
+                    __hip_atomic_store(ring_turn(seq), 2u * lap + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {  // the record was never written: poison the slot it names (if in range) and skip it
+                    poison(samples, tq.rec[4u * (size_t)rec + 3u].z, n_slots);
+                    live = false;
+                }
             }
         } else {  // new paths
             const uint32_t qc = __builtin_amdgcn_readfirstlane(b) >> 6;
@@ -430,12 +447,15 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             const bool deferred = bounce_loop_r<kStats>(
                 sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
                 defer_from, job.defer_lanes, [&]() { return ring_reserve(seq); });
-            if (overflow) atomicOr(err, 1u);
+            if (overflow) atomicOr(err, kErrStack);
             if (deferred) {
                 const uint32_t lap = ring_lap(seq);
-                ring_wait(ring_turn(seq), 2u * lap, err);
-                tail_store(tq, blockIdx.x * kTailRing + seq % kTailRing, p, slot);
-                __hip_atomic_store(ring_turn(seq), 2u * lap + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (ring_wait(ring_turn(seq), 2u * lap, err, job.ring_spin)) {
+                    tail_store(tq, blockIdx.x * kTailRing + seq % kTailRing, p, slot);
+                    __hip_atomic_store(ring_turn(seq), 2u * lap + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    poison(samples, slot, n_slots);
+                }
             } else {
                 const F3 s = path_value(p);
                 samples[slot] = make_float4(s.x, s.y, s.z, 0.0f);
@@ -561,8 +581,10 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
 // last wave to finish re-zeroes the words, so the next launch needs no memset
 // -- a fill kernel queued between two frames on another stream would wait for
 // free CUs and serialise overlapping frames).
+// The last wave also publishes the launch's error flag into its status word
+// (TileJob::status) and clears the flag for the next launch on the stream.
 __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chunks, unsigned long long t_entry,
-                                                uint32_t* counter) {
+                                                uint32_t* counter, uint32_t* err) {
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (wid < job.wave_ts_cap) {
@@ -582,8 +604,22 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
         if (atomicAdd(counter + 1, 1u) == total - 1) {
             atomicExch(counter, 0u);
             atomicExch(counter + 1, 0u);
+            if (job.status) {
+                const uint32_t e = atomicExch(err, 0u);
+                __hip_atomic_store(job.status, e | kStatusDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
+}
+
+__global__ void k_publish_status(uint32_t* err, uint32_t* status) {
+    const uint32_t e = atomicExch(err, 0u);
+    __hip_atomic_store(status, e | kStatusDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s) {
+    hipLaunchKernelGGL(k_publish_status, dim3(1), dim3(1), 0, s, err, status);  // one lane
+    return hipGetLastError();
 }
 
 // 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
@@ -597,6 +633,7 @@ __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, Tile
         for (uint32_t i = threadIdx.x; i < 4u + kTailRing; i += blockDim.x) ring_ctl()[i] = 0u;
         __syncthreads();
     }
+    if (job.fault == 1u && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, kErrInjected);
 #ifdef MM_PHASE_CLOCKS
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
 #else
@@ -608,7 +645,7 @@ __global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, Tile
         else
             return wavepersist_body<kStats>(sc, q, job, samples, stats, err, work);
     });
-    persistent_exit(job, chunks, t_entry, work);
+    persistent_exit(job, chunks, t_entry, work, err);
 }
 
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
@@ -652,17 +689,35 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
 }
 
 // (LDS mode, form) pairs; the tail-deferral variant (MM_OPT_DEFER) is built
-// for the grid search and the lean BVH form with records in LDS
+// for the grid search and the lean BVH form with records in LDS.  The
+// default build holds what MM_PIPE_AUTO can select (the grid search, and the
+// BVH forms for scenes the grid cannot take: nodes + records in LDS, nodes
+// only, nothing); the A/B-only placements -- split node cache (6), nodes
+// with global records (7), dictionary nodes (10), loop form 0 -- and the
+// one-thread-per-path kernel are built with `make EXTRA=-DMM_AB_VARIANTS`
+// (mm_version() then ends in "+ab"; every one measured slower).
 #define MM_DEFER_INSTANCES(X)                                                                                 \
     X(11, kFormGrid) X(12, kFormGrid) X(13, kFormGrid)                                                        \
     X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
     X(11, kFormGridWide) X(13, kFormGridWide) X(11, kFormGridWideSlow) X(13, kFormGridWideSlow)               \
     X(3, kFormLean)
+#ifdef MM_AB_VARIANTS
 #define MM_WP_INSTANCES(X)                                                                                    \
     MM_DEFER_INSTANCES(X) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                    \
     X(0, kFormLeafInterior) X(1, kFormLeafInterior) X(3, kFormLeafInterior) X(6, kFormLeafInterior)           \
     X(7, kFormLeafInterior) X(10, kFormLeafInterior)                                                          \
     X(1, kFormIfIf) X(3, kFormIfIf)
+#else
+#define MM_WP_INSTANCES(X)                                                                                    \
+    MM_DEFER_INSTANCES(X) X(0, kFormLeafInterior) X(1, kFormLeafInterior) X(3, kFormLeafInterior)
+#endif
+
+bool wavepersist_built(int lds_mode, int form) {
+#define MM_WP(L, F) if (lds_mode == L && form == F) return true;
+    MM_WP_INSTANCES(MM_WP)
+#undef MM_WP
+    return false;
+}
 
 bool wavepersist_defer_built(int lds_mode, int form) {
 #define MM_WP(L, F) if (lds_mode == L && form == F) return true;
@@ -688,6 +743,20 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
     return hipErrorInvalidValue;
 }
 
+hipError_t wavepersist_attributes(int lds_mode, int form, bool defer, hipFuncAttributes* a) {
+#define MM_WP(L, F)                                                                                          \
+    if (lds_mode == L && form == F && defer)                                                                 \
+        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, true>));
+    MM_DEFER_INSTANCES(MM_WP)
+#undef MM_WP
+#define MM_WP(L, F)                                                                                          \
+    if (lds_mode == L && form == F && !defer)                                                                \
+        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, false>));
+    MM_WP_INSTANCES(MM_WP)
+#undef MM_WP
+    return hipErrorInvalidValue;
+}
+
 template <bool kRef, bool kLds>
 static void launch_mega_t(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
                           uint32_t* err, bool count_stats, uint32_t block, hipStream_t s) {
@@ -702,13 +771,27 @@ static void launch_mega_t(const DevScene& sc, const TileJob& job, float4* sample
 
 hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats_dev,
                              uint32_t* err, bool count_stats, const MegaOpts& o, hipStream_t s) {
-    if (o.reference)
+    if (o.reference) {
         launch_mega_t<true, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
-    else if (o.lds_nodes)
+        return hipGetLastError();
+    }
+#ifdef MM_AB_VARIANTS
+    if (o.lds_nodes)
         launch_mega_t<false, true>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
     else
         launch_mega_t<false, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
     return hipGetLastError();
+#else
+    return hipErrorInvalidValue;  // one thread per path: A/B build only
+#endif
+}
+
+bool ab_variants_built() {
+#ifdef MM_AB_VARIANTS
+    return true;
+#else
+    return false;
+#endif
 }
 
 // ---------------------------------------------------------------------------

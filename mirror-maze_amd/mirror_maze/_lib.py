@@ -35,11 +35,13 @@ MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE = 0x1, 0x2
 MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2, 3
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS = 1, 2, 3, 7, 8
 MM_OPT_LDS_SPLIT, MM_OPT_FUSE_RESOLVE, MM_OPT_RESERVE_CUS, MM_OPT_DICT_NODES, MM_OPT_DEFER = 9, 12, 19, 20, 21
-MM_OPT_DEFER_MIN = 22
+MM_OPT_DEFER_MIN, MM_OPT_FAULT_INJECT = 22, 23
+MM_PENDING = 1
 MM_TRAV_AUTO, MM_TRAV_IFIF, MM_TRAV_LEAF_INTERIOR, MM_TRAV_LEAN, MM_TRAV_GRID = -1, 0, 5, 7, 11
 MM_INFO_GRID_OK, MM_INFO_GRID_CELLS_X, MM_INFO_GRID_CELLS_Y, MM_INFO_GRID_CELLS_Z = 1, 2, 3, 4
 MM_INFO_GRID_GLOBAL, MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_LEAN, MM_INFO_DEPTH = 5, 6, 7, 8, 9
 MM_INFO_DICT_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE, MM_INFO_GRID_FACES = 10, 11, 12, 13
+MM_INFO_LAST_DEFER, MM_INFO_LAST_VGPRS, MM_INFO_LAST_SCRATCH, MM_INFO_LAST_STATIC_LDS = 14, 15, 16, 17
 MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
@@ -114,6 +116,8 @@ EXPORTS = {
     "mm_scene_info": (C.c_int, [P, C.c_int, C.POINTER(C.c_double)]),
     "mm_set_wave_timeline": (C.c_int, [P, P, C.c_uint32]),
     "mm_sync": (C.c_int, [P]),
+    "mm_last_call": (C.c_int, [P, C.POINTER(C.c_uint64)]),
+    "mm_call_status": (C.c_int, [P, C.c_uint64]),
     "mm_last_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
     "mm_set_profiling": (C.c_int, [P, C.c_int]),
     "mm_kernel_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_int]),
@@ -164,6 +168,11 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def ab_variants() -> bool:
+    """True when the library was built with -DMM_AB_VARIANTS (A/B-only kernels)."""
+    return lib().mm_version().decode().endswith("+ab")
 
 
 def check(rc: int, ctx=None) -> None:

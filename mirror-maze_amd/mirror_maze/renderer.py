@@ -191,7 +191,25 @@ class Renderer:
         return out, (st if stats else None)
 
     def sync(self) -> None:
+        """Wait for this context's work; raises MMError for the oldest
+        trace_tile* call that failed on the GPU and was not reported yet (the
+        message names that call)."""
         self._check(lib().mm_sync(self._ctx))
+
+    def last_call(self) -> int:
+        """Number of the last trace_tile / trace_tile_frames call (1, 2, ...)."""
+        n = C.c_uint64()
+        self._check(lib().mm_last_call(self._ctx, C.byref(n)))
+        return n.value
+
+    def call_status(self, call_id: int) -> bool:
+        """Without waiting: True if call `call_id` finished clean, False while
+        it runs; raises MMError (naming the call) if it failed on the GPU."""
+        rc = lib().mm_call_status(self._ctx, call_id)
+        if rc == _lib.MM_PENDING:
+            return False
+        self._check(rc)
+        return True
 
     def set_profiling(self, enable: bool = True) -> None:
         self._check(lib().mm_set_profiling(self._ctx, 1 if enable else 0))

@@ -63,15 +63,18 @@ def host_threads() -> int:
     return max(1, min(16, n))
 
 
-def oracle_tile(o, uniform, ext, x0, y0, w, h, y_stride=1, threads=None):
+def oracle_tile(o, uniform, ext, x0, y0, w, h, y_stride=1, threads=None, out=None):
     """oracle_trace_tile over a thread pool (the C call releases the GIL): the
     tile's rows in bands, bit-identical to one call (each pixel's value
-    depends on its own (pixel, sample, frame) only).  Returns (out, rays)."""
+    depends on its own (pixel, sample, frame) only).  `out` (h, w, 4) float32
+    receives the tile (with MM_EXT_ACCUMULATE: adds into it).  Returns (out,
+    rays)."""
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
 
     threads = threads or host_threads()
-    out = np.zeros((h, w, 4), dtype=np.float32)
+    if out is None:
+        out = np.zeros((h, w, 4), dtype=np.float32)
     band = max(1, -(-h // (4 * threads)))
     jobs = [(j0, min(band, h - j0)) for j0 in range(0, h, band)]
 

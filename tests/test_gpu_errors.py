@@ -1,0 +1,209 @@
+"""Errors raised on the GPU reach the caller, attributed to the call that
+caused them, and valid long paths raise none.
+
+* Long chunks with the tail rings: a bounce limit of 32767 (the largest the
+  API takes) with deferral forced makes every chunk run far longer than the
+  round-2 drain bound (2^21 polls of s_sleep(2), ~0.13 s); the launch must end
+  clean and bit-exact against the oracle.  The loop whose length nothing may
+  cap is src/shaders.metal:306 (`n < bounce_limit + mirror_hits`).
+* An injected fault (MM_OPT_FAULT_INJECT 1) is reported naming its own call
+  -- by mm_sync, by the next trace call (which is then not enqueued) and by
+  mm_call_status -- never blamed on a later call.
+* Ring protocol timeouts (MM_OPT_FAULT_INJECT 2: waits give up at once) are
+  reported, and the samples they skipped are NaN in the image."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import oracle_tile
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _scene(n):
+    from mirror_maze import Scene
+
+    return Scene.build(n, 0)
+
+
+def test_long_chunks_with_tail_rings_end_clean_and_bit_exact(gpu):
+    """Round 2's drain gave up after 2^21 polls of s_sleep(2) (>= 2^21 x 128
+    clocks = 0.11 s at 2.4 GHz, ~0.13 s with the poll's LDS reads) although a
+    block-mate's valid chunk may run bounce_limit + mirror_limit iterations.
+    Here every chunk does: half the walls are mirrors, so a path runs until
+    it has 32766 mirror hits or 32767 + its mirror hits bounces (~65 k
+    iterations); the camera sits inside the closed maze; one resident block
+    (1024 paths = 16 chunks, so 16 busy waves share one CU) reads the grid
+    through L1/L2.  The longest chunk must outlast the old bound several
+    times over, and the launch must end clean and bit-exact."""
+    import torch
+
+    from mirror_maze import MM_INFO_LAST_DEFER, Renderer, Scene, calculate_quaternion, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    base = _scene(32)
+    rng = np.random.default_rng(5)
+    mirror = (rng.random(base.n_rects) < 0.5).astype(np.uint8)
+    s = Scene(base.maze_n, base.rects, base.nodes, base.idx, mirror, base.emission, base.grid, base.bvh_depth)
+    r = Renderer(0)
+    r.set_option(1, 0)    # MM_OPT_LDS_NODES 0: the grid image through L1/L2 (LDS mode 13, deferral built)
+    r.set_option(21, 32)  # MM_OPT_DEFER: 32 lanes
+    r.set_option(22, 0)   # MM_OPT_DEFER_MIN: any launch size
+    r.upload_scene(s)
+    u = default_uniform(320, 180, 0)
+    u.cam.center[0] = -160.0 + 10.0 * 16 + 5.0
+    u.cam.center[1] = 0.0
+    u.cam.center[2] = -160.0 + 10.0 * 16 + 5.0
+    q = calculate_quaternion(np.asarray((-0.3, -0.1, 1.0), dtype=np.float32))
+    for i in range(4):
+        u.cam.quat[i] = float(q[i])
+    e = make_ext(8, 32767, 32767, frame=1)
+    ts = torch.zeros((256 * 2 * 16, 4), dtype=torch.int64, device="cuda")
+    r.set_wave_timeline(ts)
+    got, st = r.trace_tile(u, e, 152, 86, 16, 8, stats=True)  # 16 x 8 px x 8 spp = 1024 paths: one block
+    r.sync()  # raises if the launch reported an error
+    r.set_wave_timeline(None)
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 1.0
+    t = ts.cpu().numpy()
+    busy = t[t[:, 3] > 0]                              # waves that traced at least one chunk
+    span_s = (busy[:, 2] - busy[:, 0]).max() / 100e6   # wall_clock64: 100 MHz
+    print(f"longest wave: {span_s:.3f} s; {len(busy)} busy waves, {int(busy[:, 3].sum())} chunks; "
+          f"{st.rays} queries ({st.rays / 1024:.0f} per path)")
+    assert span_s > 0.3, span_s
+    ref, rays = oracle_tile(Oracle.from_scene(s), u, e, 152, 86, 16, 8)
+    assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref))
+    assert st.rays == rays
+    r.close()
+
+
+def test_injected_fault_is_reported_by_the_call_that_caused_it(gpu):
+    from mirror_maze import MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.upload_scene(_scene(10))
+    u = default_uniform(256, 128, 0)
+    e = make_ext(8, 8, 8)
+    # 1. a clean call, then a faulting one, then mm_sync names the faulting call
+    r.trace_tile(u, e, 0, 0, 256, 128)
+    ok = r.last_call()
+    r.set_option(23, 1)
+    r.trace_tile(u, e, 0, 0, 256, 128)  # returns at once: the fault happens on the GPU
+    bad = r.last_call()
+    r.set_option(23, 0)
+    assert bad == ok + 1
+    with pytest.raises(MMError) as ei:
+        r.sync()
+    assert f"call #{bad} " in str(ei.value) and "injected fault" in str(ei.value)
+    assert r.call_status(ok) is True
+    r.sync()  # reported once: the context is clean again
+    # 2. the next trace call reports a failed earlier call and is not enqueued
+    r.set_option(23, 1)
+    r.trace_tile(u, e, 0, 0, 256, 128)
+    bad2 = r.last_call()
+    r.set_option(23, 0)
+    import torch
+
+    torch.cuda.synchronize()  # let it finish (the status words need no mm_sync)
+    with pytest.raises(MMError) as ei:
+        r.trace_tile(u, e, 0, 0, 256, 128)
+    assert f"call #{bad2} " in str(ei.value) and "not enqueued" in str(ei.value)
+    assert r.last_call() == bad2  # the refused call got no number
+    with pytest.raises(MMError):  # mm_call_status keeps naming it
+        r.call_status(bad2)
+    img, _ = r.trace_tile(u, e, 0, 0, 256, 128)
+    r.sync()
+    assert r.call_status(r.last_call()) is True and np.isfinite(img.cpu().numpy()).all()
+    # 3. with stats the call syncs and reports its own fault directly
+    r.set_option(23, 1)
+    with pytest.raises(MMError) as ei:
+        r.trace_tile(u, e, 0, 0, 256, 128, stats=True)
+    assert f"call #{r.last_call()} " in str(ei.value)
+    r.set_option(23, 0)
+    r.close()
+
+
+def test_pending_status_is_visible_without_waiting(gpu):
+    """mm_call_status does not block: a long call reads as pending, then clean."""
+    import time
+
+    from mirror_maze import Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.upload_scene(_scene(32))
+    u = default_uniform(1920, 1080, 0)
+    r.trace_tile_frames(u, make_ext(8, 8, 8), 8, 0, 0, 1920, 1080)  # ~25 ms of GPU work
+    c = r.last_call()
+    first = r.call_status(c)
+    t0 = time.time()
+    while not r.call_status(c):
+        assert time.time() - t0 < 30
+        time.sleep(0.001)
+    assert first is False  # seen running before it ended
+    r.sync()
+    r.close()
+
+
+def test_ring_timeouts_are_reported_and_poison_the_skipped_samples(gpu):
+    from mirror_maze import MMError, Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(32)
+    r = Renderer(0)
+    r.set_option(21, 64)  # every path defers at bounce 1: the rings run full
+    r.set_option(22, 0)
+    r.upload_scene(s)
+    u = default_uniform(256, 144, 0)
+    e = make_ext(8, 8, 8, frame=0)
+    r.set_option(23, 2)   # protocol waits give up at once
+    got, _ = r.trace_tile(u, e, 0, 0, 256, 144)
+    call = r.last_call()
+    r.set_option(23, 0)
+    try:
+        r.sync()
+        failed = False
+    except MMError as ex:
+        failed = True
+        assert f"call #{call} " in str(ex) and "tail ring wait timed out" in str(ex)
+    img = got.cpu().numpy()
+    if failed:
+        assert np.isnan(img[..., :3]).any()  # a skipped sample shows in its pixel
+    else:  # no wait was ever needed: the image is exact
+        ref, _ = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 256, 144)
+        assert np.array_equal(_bits(img), _bits(ref))
+    # the context works normally afterwards
+    again, _ = r.trace_tile(u, e, 0, 0, 256, 144)
+    r.sync()
+    assert np.isfinite(again.cpu().numpy()).all()
+    r.close()
+
+
+def test_staging_bound_for_multi_frame_launches(gpu):
+    """staged samples are bounded at 2^29 paths (8 GiB) per launch.
+    A multi-frame launch over it runs with the fused resolve when it can
+    (MM_INFO_LAST_DEFER 0, frames bit-identical to single-frame launches) and
+    is refused otherwise; a single frame over it is split into row batches."""
+    import torch
+
+    from mirror_maze import MM_INFO_LAST_DEFER, MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.upload_scene(_scene(16))
+    u = default_uniform(1920, 1080, 0)
+    # 1920 x 1080 x 8 spp x 33 frames = 547 M staged paths > 2^29: fused resolve instead of the rings
+    n = 33
+    many, _ = r.trace_tile_frames(u, make_ext(8, 8, 8, frame=0), n, 0, 0, 1920, 1080)
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 0.0
+    for f in (0, n - 1):
+        one, _ = r.trace_tile(u, make_ext(8, 8, 8, frame=f), 0, 0, 1920, 1080)
+        assert torch.equal(one.view(torch.int32), many[f].view(torch.int32)), f
+    del many
+    # 3 spp cannot fuse: 1920 x 1080 x 3 x 87 frames > 2^29 is refused before any launch
+    with pytest.raises(MMError):
+        r.trace_tile_frames(u, make_ext(3, 8, 8), 87, 0, 0, 1920, 1080)
+    r.sync()
+    r.close()

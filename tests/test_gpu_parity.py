@@ -137,9 +137,24 @@ PIPES = {
 }
 
 
+# Variants built only with `make EXTRA=-DMM_AB_VARIANTS`: the
+# default library holds the kernels MM_PIPE_AUTO can select.
+AB_ONLY = {"mega-global", "mega-lds", "bvh-lean-globalrecs", "bvh-lean-split2kb", "bvh-lean-dict",
+           "bvh-li-split2kb", "bvh-li-dict", "bvh-ifif-ldsrects", "bvh-ifif-lds"}
+
+
+def _need_ab(what):
+    from mirror_maze import ab_variants
+
+    if not ab_variants():
+        pytest.skip(f"{what}: A/B-only variant (library built without -DMM_AB_VARIANTS)")
+
+
 def _renderer(pipe, scene):
     from mirror_maze import Renderer
 
+    if pipe in AB_ONLY:
+        _need_ab(pipe)
     r = Renderer(0)
     p, opts, _ = PIPES[pipe]
     r.set_pipeline(p)
@@ -232,6 +247,8 @@ def test_multi_frame_launch_bit_identical(gpu, opts):
 
     from mirror_maze import Renderer, default_uniform, make_ext
 
+    if opts.get(9, 0) > 1:
+        _need_ab("split node cache")
     s = _scene(32)
     r = Renderer(0)
     for k, v in opts.items():
@@ -357,6 +374,10 @@ def test_large_scene_bit_exact(gpu, opts):
     from mirror_maze import MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_GRID_OK, default_uniform, make_ext
     from oracle.oracle import Oracle
 
+    dict_auto = opts.get(7) == 5 and opts.get(20, 1) and opts.get(9, 1) and opts.get(1, 1)  # "li-dict"
+    if opts.get(9, 0) > 1 or opts.get(3) == 0 or opts.get(7) == 7 or dict_auto:
+        _need_ab("N=64 BVH placement (dictionary nodes, split cache, lean form with global records, "
+                 "one thread per path)")
     s = _scene(64)
     assert s.n_nodes * 32 > 160 * 1024
     o = Oracle.from_scene(s)
@@ -414,6 +435,10 @@ def test_bench_prints_one_json_line(gpu):
     assert d["unit"] == "Mrays/s" and d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2
     assert d["roofline"]["bound"] == "valu" and 0 < d["roofline"]["frac"] < 1
     assert d["roofline"]["model_hbm"]["bytes_per_ray"] == 136 and "measured" in d["roofline"]
+    assert 0 < d["roofline"]["reference_equivalent"]["frac"] < 1 and d["roofline"]["basis"]
+    kr = d["roofline"]["kernel_resources"]
+    assert 0 < kr["vgprs_per_lane"] <= 64 and kr["scratch_bytes_per_lane"] >= 0
+    assert d["distributed"] is None  # one process, no torchrun
     assert d["config"]["frame_contexts"] in (1, 2)
     assert d["config"]["frames_per_launch"] == 2  # default batching: the 2 timed frames in one launch
     assert d["roofline"]["launches"] == 1

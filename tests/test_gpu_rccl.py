@@ -76,6 +76,15 @@ def test_bench_distributed_path_delivers_the_frame(gpu, tmp_path, config):
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][-1])
     assert line["n_gpus"] == 1 and line["config"]["frame_format"] == "rgba8"
     assert "RCCL" in line["config"]["parallelism"]
+    # the multi-GPU instrumentation, consistent at N = 1
+    d = line["distributed"]
+    assert d["rccl_world"] == 1 and d["backend"] == "nccl"
+    k = d["kernel_ms_per_rank"]
+    assert k["min"] == k["max"] == k["rank0"] > 0
+    assert abs(k["rank0"] - line["roofline"]["kernel_avg_ms"] * line["roofline"]["launches"]) < 0.01
+    g = d["exposed_gather_ms"]
+    assert 0 <= g["rank0"] <= g["max"] <= line["ms_per_step"] * steps
+    assert d["frames_per_gather"] == line["config"]["frames_per_launch"] and d["gathers_total"] >= 1
     got = np.load(out)
     maze_n, W, H, spp, bl, ml, _ = CONFIGS[config]
     r = Renderer(0)
