@@ -196,6 +196,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   default 2^24: below it the staged resolve outweighs the tail saved -- C1
                                   0.039 vs 0.033 ms/frame, C2 x 5 frames 0.49 vs 0.42; 10 frames of rank 0 of an
                                   8-way C3 split, 20.7 M paths, 0.50 vs 0.51); 0: always */
+#define MM_OPT_GRID_MERGE 24  /* grid search: 1 (default) an axis whose cells would not shorten the lists
+                                  gets one cell (the maze: one cell along y -- its walls span the height, the
+                                  lower cell is the space below the floor); 0 cells per axis by the typical
+                                  rect size only.  Read by mm_upload_scene */
 #define MM_OPT_FAULT_INJECT 23 /* tests of the error path (results are then invalid): 0 off (default); 1 every
                                   wave-persistent launch raises an injected fault (error bit 3); 2 the tail
                                   rings' protocol waits give up at once (bit 2 when a wait was needed; the

@@ -121,42 +121,98 @@ uint32_t grid_records(const std::vector<uint32_t>& rc, uint32_t n_rects, std::ve
 // Cells of size ~s over the scene box widened by eps = C * 2^-14, their lists
 // and the image layout (recs and boxes are filled by the caller).
 bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint32_t>& recs, const double smin[3],
-                 const double smax[3], double C, double s, bool wide, GridHost& g, std::string& why) {
+                 const double smax[3], double C, double s, bool wide, bool merge_axes, GridHost& g,
+                 std::string& why) {
     g.wide = wide;
     g.n_glob = 0;
     const double eps = C * 0x1p-14;
     long total = 1;
-    for (int a = 0; a < 3; ++a) {
+    auto set_axis = [&](int a, int n) {
         const float lo = std::nextafter((float)(smin[a] - eps), -INFINITY);
         const float hi = std::nextafter((float)(smax[a] + eps), INFINITY);
-        int n = (int)std::floor(((double)hi - lo) / s + 0.5);
-        n = std::max(1, std::min(256, n));
         g.n[a] = n;
         g.mn[a] = lo;
         g.mx[a] = hi;
         g.cell[a] = (float)(((double)hi - lo) / n);
         g.inv[a] = 1.0f / g.cell[a];
-        total *= n;
+    };
+    for (int a = 0; a < 3; ++a) {
+        const double ext = (double)std::nextafter((float)(smax[a] + eps), INFINITY) -
+                           std::nextafter((float)(smin[a] - eps), -INFINITY);
+        set_axis(a, std::max(1, std::min(256, (int)std::floor(ext / s + 0.5))));
+        total *= g.n[a];
     }
     if (total > (1l << 20)) { why = "more than 2^20 cells"; return false; }
     // cell ranges of every rect (widened by eps), global rects
     struct Span { int i0[3], i1[3]; long cover; };
     std::vector<Span> span(n_rects);
     std::vector<uint8_t> skip(n_rects, 0), glob(n_rects, 0);
-    std::vector<std::pair<long, uint32_t>> big;
-    for (uint32_t k = 0; k < n_rects; ++k) {
-        skip[k] = (recs[10 * (size_t)k + 9] >> 30) == 1u;
-        double lo[3], hi[3];
-        rect_box(rects[k], lo, hi);
-        Span& sp = span[k];
-        sp.cover = 1;
-        for (int a = 0; a < 3; ++a) {
-            sp.i0[a] = std::max(0, (int)std::floor((lo[a] - eps - g.mn[a]) / g.cell[a]));
-            sp.i1[a] = std::min(g.n[a] - 1, (int)std::floor((hi[a] + eps - g.mn[a]) / g.cell[a]));
-            sp.cover *= std::max(0, sp.i1[a] - sp.i0[a] + 1);
+    auto spans = [&]() {
+        for (uint32_t k = 0; k < n_rects; ++k) {
+            skip[k] = (recs[10 * (size_t)k + 9] >> 30) == 1u;
+            double lo[3], hi[3];
+            rect_box(rects[k], lo, hi);
+            Span& sp = span[k];
+            sp.cover = 1;
+            for (int a = 0; a < 3; ++a) {
+                sp.i0[a] = std::max(0, (int)std::floor((lo[a] - eps - g.mn[a]) / g.cell[a]));
+                sp.i1[a] = std::min(g.n[a] - 1, (int)std::floor((hi[a] + eps - g.mn[a]) / g.cell[a]));
+                sp.cover *= std::max(0, sp.i1[a] - sp.i0[a] + 1);
+            }
         }
-        if (!skip[k] && sp.cover * 2 > total) big.push_back({sp.cover, k});
+    };
+    spans();
+    // An axis whose cells do not shorten the lists gets one cell: when the
+    // listed rects span (nearly) all of its cells -- the maze's walls span its
+    // whole height -- splitting it only adds cell steps (C3: 2.13 -> 1.91 cell
+    // steps per query at the same 4.4 rect tests, scripts/grid_sim.c NY=1;
+    // the search and its proof are the same for any cell counts).
+    // Criterion: merging the axis does not lengthen the longest list among the
+    // cells it merges (summed over the merged cells, within 10 %) -- the
+    // maze's lower y cell is the space below the floor and lists a subset of
+    // the walls above it, which a ray enters only to find that the floor hit
+    // just below the boundary was its answer.
+    for (int a = 0; merge_axes && a < 3; ++a) {
+        if (g.n[a] == 1) continue;
+        std::vector<uint32_t> split(total, 0), merged(total / g.n[a], 0);
+        for (uint32_t k = 0; k < n_rects; ++k) {
+            const Span& sp = span[k];
+            if (skip[k] || sp.cover * 2 > total) continue;  // (the global rects are tested by every query)
+            for (int z = sp.i0[2]; z <= sp.i1[2]; ++z)
+                for (int y = sp.i0[1]; y <= sp.i1[1]; ++y)
+                    for (int x = sp.i0[0]; x <= sp.i1[0]; ++x) {
+                        split[((long)z * g.n[1] + y) * g.n[0] + x]++;
+                        const int q[3] = {x, y, z};
+                        if (q[a] != sp.i0[a]) continue;  // once per merged cell
+                        int m[3] = {x, y, z};
+                        m[a] = 0;
+                        int nm[3] = {g.n[0], g.n[1], g.n[2]};
+                        nm[a] = 1;
+                        merged[((long)m[2] * nm[1] + m[1]) * nm[0] + m[0]]++;
+                    }
+        }
+        double longest = 0.0, union_len = 0.0;
+        for (long c = 0; c < total; ++c) {
+            const int q[3] = {(int)(c % g.n[0]), (int)((c / g.n[0]) % g.n[1]), (int)(c / ((long)g.n[0] * g.n[1]))};
+            if (q[a] != 0) continue;
+            int step[3] = {1, g.n[0], g.n[0] * g.n[1]};
+            uint32_t mx = 0;
+            for (int i = 0; i < g.n[a]; ++i) mx = std::max(mx, split[c + (long)i * step[a]]);
+            longest += mx;
+            int m[3] = {q[0], q[1], q[2]};
+            int nm[3] = {g.n[0], g.n[1], g.n[2]};
+            nm[a] = 1;
+            union_len += merged[((long)m[2] * nm[1] + m[1]) * nm[0] + m[0]];
+        }
+        if (union_len <= 1.1 * longest) {
+            total /= g.n[a];
+            set_axis(a, 1);
+            spans();
+        }
     }
+    std::vector<std::pair<long, uint32_t>> big;
+    for (uint32_t k = 0; k < n_rects; ++k)
+        if (!skip[k] && span[k].cover * 2 > total) big.push_back({span[k].cover, k});
     std::sort(big.begin(), big.end(), [](auto& x, auto& y) { return x.first > y.first; });
     for (size_t i = 0; i < big.size() && i < 4; ++i) {
         glob[big[i].second] = 1;
@@ -282,7 +338,7 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
 // extent and grows by 1.25x until the cells + lists (the part the kernel keeps
 // in LDS) fit index_budget bytes.
 bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
-                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why) {
+                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why, bool merge_axes) {
     if (n_rects == 0 || n_rects > 65535) { why = "rect count outside 1..65535"; return false; }
     std::vector<uint32_t> ident(n_rects), recs;
     for (uint32_t k = 0; k < n_rects; ++k) ident[k] = k;
@@ -312,8 +368,12 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         // 64-bit cell words with face ranges where the whole image fits the
         // budget, else plain 32-bit words at the same cell size, before
         // coarser cells (the kernel variant for wide words stages all of it)
-        if (build_lists(rects, n_rects, recs, smin, smax, C, s, true, g, why) && g.bytes <= index_budget) break;
-        if (build_lists(rects, n_rects, recs, smin, smax, C, s, false, g, why) && g.off_recs <= index_budget) break;
+        if (build_lists(rects, n_rects, recs, smin, smax, C, s, true, merge_axes, g, why) &&
+            g.bytes <= index_budget)
+            break;
+        if (build_lists(rects, n_rects, recs, smin, smax, C, s, false, merge_axes, g, why) &&
+            g.off_recs <= index_budget)
+            break;
         if (attempt == 23) { why = "no grid index fits the LDS budget"; return false; }
     }
     std::vector<uint32_t> grecs;

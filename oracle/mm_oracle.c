@@ -14,6 +14,37 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <xmmintrin.h>
+
+/* ---- floating-point environment (TEST INFRASTRUCTURE) -----------------------
+ * The reference AIR is compiled with `air.compile.denorms_disable`
+ * (src/shaders.ir metadata !47): denormal operands read as zero and denormal
+ * results flush to zero.  The oracle runs IEEE binary32 (denormals kept) by
+ * default, like the HIP kernels; oracle_set_fp_mode(1) runs every entry point
+ * with MXCSR FTZ|DAZ (the reference's semantics) instead.  Every entry point
+ * also ORs the MXCSR sticky exception flags it raised (bit 1 DE: a denormal
+ * operand; bit 4 UE: a tiny inexact result) into oracle_fp_flags(), so a run
+ * shows whether any denormal arose at all. */
+static int g_fp_ftz = 0;
+static unsigned g_fp_flags = 0;
+void oracle_set_fp_mode(int ftz_daz) { g_fp_ftz = ftz_daz != 0; }
+unsigned oracle_fp_flags(int reset) {
+    unsigned f = __atomic_load_n(&g_fp_flags, __ATOMIC_RELAXED);
+    if (reset) __atomic_store_n(&g_fp_flags, 0u, __ATOMIC_RELAXED);
+    return f;
+}
+static unsigned fp_enter(void) {
+    const unsigned saved = _mm_getcsr();
+    unsigned csr = saved & ~0x3Fu;                  /* clear the sticky flags */
+    if (g_fp_ftz) csr |= (1u << 15) | (1u << 6);    /* FTZ | DAZ */
+    else csr &= ~((1u << 15) | (1u << 6));
+    _mm_setcsr(csr);
+    return saved;
+}
+static void fp_leave(unsigned saved) {
+    __atomic_fetch_or(&g_fp_flags, _mm_getcsr() & 0x3Fu, __ATOMIC_RELAXED);
+    _mm_setcsr(saved);
+}
 
 #define BIG 1e30f          /* IR 0x46293E5940000000 */
 #define STACK_MAX 50       /* shaders.metal:123 */
@@ -257,7 +288,7 @@ static v3 jittered_dir(v3 d, uint32_t* seed) {
     return vadd(d, j);                                        /* %192 */
 }
 
-int oracle_trace_path(const oracle_scene* sc, const float ori[3], const float dir[3],
+static int oracle_trace_path_body(const oracle_scene* sc, const float ori[3], const float dir[3],
                       uint32_t seed, int bounce_limit, int mirror_limit,
                       float rgb_out[3], uint32_t* rays) {
     uint64_t nr = 0;
@@ -267,6 +298,16 @@ int oracle_trace_path(const oracle_scene* sc, const float ori[3], const float di
     if (rays) *rays = (uint32_t)nr;
     return tr.overflow ? MM_ERR_STACK : MM_OK;
 }
+
+int oracle_trace_path(const oracle_scene* sc, const float ori[3], const float dir[3],
+                      uint32_t seed, int bounce_limit, int mirror_limit,
+                      float rgb_out[3], uint32_t* rays) {
+    const unsigned saved = fp_enter();
+    const int rc = oracle_trace_path_body(sc, ori, dir, seed, bounce_limit, mirror_limit, rgb_out, rays);
+    fp_leave(saved);
+    return rc;
+}
+
 
 static void add_stats(mm_stats* st, uint64_t rays, const trav_t* tr, uint64_t paths) {
     if (!st) return;
@@ -332,7 +373,7 @@ static int check_group_shape(const mm_uniform* u, uint32_t tg_w, uint32_t tg_h) 
     return MM_OK;
 }
 
-int oracle_trace_group(const oracle_scene* sc, const mm_uniform* u, const uint32_t* chunks,
+static int oracle_trace_group_body(const oracle_scene* sc, const mm_uniform* u, const uint32_t* chunks,
                        uint32_t n_chunks, uint32_t tg_w, uint32_t tg_h, uint32_t gx, uint32_t gy,
                        float* fb, mm_stats* st) {
     int rc = check_group_shape(u, tg_w, tg_h);
@@ -341,7 +382,17 @@ int oracle_trace_group(const oracle_scene* sc, const mm_uniform* u, const uint32
     return run_group(sc, u, chunks, n_chunks, tg_w, tg_h, gx, gy, fb, st, test);
 }
 
-int oracle_trace_chunks(const oracle_scene* sc, const mm_uniform* u, const uint32_t* chunks,
+int oracle_trace_group(const oracle_scene* sc, const mm_uniform* u, const uint32_t* chunks,
+                       uint32_t n_chunks, uint32_t tg_w, uint32_t tg_h, uint32_t gx, uint32_t gy,
+                       float* fb, mm_stats* st) {
+    const unsigned saved = fp_enter();
+    const int rc = oracle_trace_group_body(sc, u, chunks, n_chunks, tg_w, tg_h, gx, gy, fb, st);
+    fp_leave(saved);
+    return rc;
+}
+
+
+static int oracle_trace_chunks_body(const oracle_scene* sc, const mm_uniform* u, const uint32_t* chunks,
                         uint32_t n_chunks, uint32_t tg_w, uint32_t tg_h, float* fb, mm_stats* st) {
     int rc = check_group_shape(u, tg_w, tg_h);
     if (rc) return rc;
@@ -358,10 +409,19 @@ int oracle_trace_chunks(const oracle_scene* sc, const mm_uniform* u, const uint3
     return MM_OK;
 }
 
+int oracle_trace_chunks(const oracle_scene* sc, const mm_uniform* u, const uint32_t* chunks,
+                        uint32_t n_chunks, uint32_t tg_w, uint32_t tg_h, float* fb, mm_stats* st) {
+    const unsigned saved = fp_enter();
+    const int rc = oracle_trace_chunks_body(sc, u, chunks, n_chunks, tg_w, tg_h, fb, st);
+    fp_leave(saved);
+    return rc;
+}
+
+
 /* Throughput mode.  Sample reduction: for spp % 8 == 0 the reference's order
  * (pairwise tree in blocks of 8, blocks summed left to right), then / spp;
  * otherwise a left-to-right sum. */
-int oracle_trace_tile(const oracle_scene* sc, const mm_uniform* u, const mm_ext* e,
+static int oracle_trace_tile_body(const oracle_scene* sc, const mm_uniform* u, const mm_ext* e,
                       uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t y_stride,
                       float* out, mm_stats* st) {
     if (!e || e->spp == 0 || e->spp > 4096 || y_stride == 0) return MM_ERR_INVALID;
@@ -406,6 +466,16 @@ int oracle_trace_tile(const oracle_scene* sc, const mm_uniform* u, const mm_ext*
     add_stats(st, rays, &tr, (uint64_t)w * h * e->spp);
     return MM_OK;
 }
+
+int oracle_trace_tile(const oracle_scene* sc, const mm_uniform* u, const mm_ext* e,
+                      uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t y_stride,
+                      float* out, mm_stats* st) {
+    const unsigned saved = fp_enter();
+    const int rc = oracle_trace_tile_body(sc, u, e, x0, y0, w, h, y_stride, out, st);
+    fp_leave(saved);
+    return rc;
+}
+
 
 /* ---- display stage (TEST INFRASTRUCTURE) -------------------------------------
  * fragment_shader (src/shaders.metal:214-225) as a Jacobi step, in the

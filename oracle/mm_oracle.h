@@ -63,6 +63,14 @@ int oracle_trace_path(const oracle_scene* sc, const float ori[3], const float di
 void oracle_present_blur(const uint8_t* in, uint8_t* out, uint32_t W, uint32_t H);
 void oracle_quantize(const float* rgba, uint8_t* rgba8, uint64_t n_pixels);
 
+/* Floating-point environment of the trace entry points: 0 IEEE binary32
+ * with denormals (default, the HIP kernels' semantics), 1 MXCSR FTZ|DAZ (the
+ * reference's `air.compile.denorms_disable`, src/shaders.ir !47).  The MXCSR
+ * sticky flags the entry points raised (bit 1 DE denormal operand, bit 4 UE
+ * underflow) accumulate in oracle_fp_flags (reset = 1 clears them). */
+void     oracle_set_fp_mode(int ftz_daz);
+unsigned oracle_fp_flags(int reset);
+
 /* Pieces exported for unit tests. */
 float    oracle_rand_pm1(uint32_t* state);          /* (random(state)-0.5)*2 */
 uint32_t oracle_seed_reference(uint32_t tx, uint32_t ty, uint32_t time);

@@ -61,6 +61,10 @@ def lib():
         L.oracle_present_blur.restype = None
         L.oracle_quantize.argtypes = [P, P, C.c_uint64]
         L.oracle_quantize.restype = None
+        L.oracle_set_fp_mode.argtypes = [C.c_int]
+        L.oracle_set_fp_mode.restype = None
+        L.oracle_fp_flags.argtypes = [C.c_int]
+        L.oracle_fp_flags.restype = C.c_uint
         _lib = L
     return _lib
 
@@ -163,3 +167,21 @@ class DisplayLoop:
         if present:
             self.tex = present_blur(self.tex)
         return self.tex
+
+
+# MXCSR sticky-flag bits oracle_fp_flags reports
+FP_DENORMAL_OPERAND, FP_UNDERFLOW = 1 << 1, 1 << 4
+
+
+def set_fp_mode(ftz_daz: bool) -> None:
+    """True: the trace entry points run with MXCSR FTZ|DAZ -- the reference's
+    `air.compile.denorms_disable` (src/shaders.ir !47); False (default): IEEE
+    binary32 with denormals, the HIP kernels' arithmetic."""
+    lib().oracle_set_fp_mode(1 if ftz_daz else 0)
+
+
+def fp_flags(reset: bool = False) -> int:
+    """MXCSR sticky flags raised by the trace entry points since the last reset
+    (FP_DENORMAL_OPERAND: some operand was denormal; FP_UNDERFLOW: some result
+    was tiny and inexact)."""
+    return int(lib().oracle_fp_flags(1 if reset else 0))

@@ -43,6 +43,8 @@ VARIANTS = {
     "defer-min0": (1, {22: 0}),     # deferral on launches of any size
     "wave": (2, {}),
     "ref": (3, {}),
+    "nomerge": (1, {24: 0}),        # MM_OPT_GRID_MERGE 0: cells along y by the rect size (round 2's grid)
+    "grid-global-nomerge": (1, {1: 0, 24: 0}),
 }
 
 

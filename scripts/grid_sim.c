@@ -102,6 +102,8 @@ static void build_grid(double cell_target) {
         if (getenv("ALIGN")) n = (int)ceil((hi - lo) / cell_target);
         if (n < 1) n = 1;
         if (n > 256) n = 256;
+        /* NY=k: force k cells along y (the maze's walls span its whole height) */
+        if (a == 1 && getenv("NY")) n = atoi(getenv("NY"));
         gn[a] = n;
         gmin[a] = (float)lo;
         gcell[a] = getenv("ALIGN") ? (float)cell_target : (float)((hi - lo) / n);

@@ -31,41 +31,61 @@ def _scene(n):
     return Scene.build(n, 0)
 
 
+def closed_room(n_tiles, mirror_frac, seed):
+    """A closed cube [-10, 10]^3 (faces overlapping at the edges: no ray from
+    inside escapes) holding n_tiles horizontal 18x18 tiles stacked along y.
+    The grid has one cell listing every tile, so every closed-hit query
+    tests them all; a fraction of the tiles are mirrors (paths run
+    bounce_limit + their mirror hits, so lanes finish at different bounces
+    and the tail rings take their last bounces)."""
+    from mirror_maze import Scene
+
+    rng = np.random.default_rng(seed)
+    rects = []
+    for sgn in (-1.0, 1.0):
+        rects.append([10 * sgn, -11, -11, 0, 22, 0, 0, 0, 22])   # x faces
+        rects.append([-11, 10 * sgn, -11, 22, 0, 0, 0, 0, 22])   # y faces
+        rects.append([-11, -11, 10 * sgn, 22, 0, 0, 0, 22, 0])   # z faces
+    for i in range(n_tiles):
+        y = -9.5 + 19.0 * (i + 0.5) / n_tiles
+        rects.append([-9, y, -9, 18, 0, 0, 0, 0, 18])
+    r = np.zeros((len(rects), 12), np.float32)
+    r[:, :9] = np.asarray(rects, np.float32)
+    r[:, 9:12] = rng.uniform(0.3, 0.9, (len(rects), 3))
+    is_mirror = np.zeros(len(rects), np.uint8)
+    is_mirror[6:] = rng.random(n_tiles) < mirror_frac
+    emission = np.tile(np.float32([1, 1, 1, 0.05]), (len(rects), 1))
+    nodes, idx = Scene.bvh(r)
+    return Scene(0, r, nodes, idx, is_mirror, emission, np.zeros((0, 0), np.uint8), 0)
+
+
 def test_long_chunks_with_tail_rings_end_clean_and_bit_exact(gpu):
     """Round 2's drain gave up after 2^21 polls of s_sleep(2) (>= 2^21 x 128
-    clocks = 0.11 s at 2.4 GHz, ~0.13 s with the poll's LDS reads) although a
-    block-mate's valid chunk may run bounce_limit + mirror_limit iterations.
-    Here every chunk does: half the walls are mirrors, so a path runs until
-    it has 32766 mirror hits or 32767 + its mirror hits bounces (~65 k
-    iterations); the camera sits inside the closed maze; one resident block
-    (1024 paths = 16 chunks, so 16 busy waves share one CU) reads the grid
-    through L1/L2.  The longest chunk must outlast the old bound several
-    times over, and the launch must end clean and bit-exact."""
+    clocks = 0.11 s at 2.4 GHz) although a block-mate's valid chunk may run
+    bounce_limit + mirror_limit iterations of arbitrarily long queries.  Here
+    one chunk (8 px x 8 spp) runs 32767 + its mirror-hit bounces in a closed
+    room where every query tests ~300 tiles, with the tail rings on; the other
+    15 waves of its block are past the global queue at once.  The chunk must
+    outlast the old bound several times over, and the launch must end clean
+    and bit-exact (the loop nothing may cap: src/shaders.metal:306)."""
     import torch
 
-    from mirror_maze import MM_INFO_LAST_DEFER, Renderer, Scene, calculate_quaternion, default_uniform, make_ext
+    from mirror_maze import MM_INFO_GRID_OK, MM_INFO_LAST_DEFER, Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 
-    base = _scene(32)
-    rng = np.random.default_rng(5)
-    mirror = (rng.random(base.n_rects) < 0.5).astype(np.uint8)
-    s = Scene(base.maze_n, base.rects, base.nodes, base.idx, mirror, base.emission, base.grid, base.bvh_depth)
+    s = closed_room(300, 0.1, 5)
     r = Renderer(0)
-    r.set_option(1, 0)    # MM_OPT_LDS_NODES 0: the grid image through L1/L2 (LDS mode 13, deferral built)
     r.set_option(21, 32)  # MM_OPT_DEFER: 32 lanes
     r.set_option(22, 0)   # MM_OPT_DEFER_MIN: any launch size
     r.upload_scene(s)
-    u = default_uniform(320, 180, 0)
-    u.cam.center[0] = -160.0 + 10.0 * 16 + 5.0
-    u.cam.center[1] = 0.0
-    u.cam.center[2] = -160.0 + 10.0 * 16 + 5.0
-    q = calculate_quaternion(np.asarray((-0.3, -0.1, 1.0), dtype=np.float32))
-    for i in range(4):
-        u.cam.quat[i] = float(q[i])
+    assert r.scene_info(MM_INFO_GRID_OK) == 1.0
+    u = default_uniform(64, 64, 0)
+    for i in range(3):
+        u.cam.center[i] = 0.0
     e = make_ext(8, 32767, 32767, frame=1)
     ts = torch.zeros((256 * 2 * 16, 4), dtype=torch.int64, device="cuda")
     r.set_wave_timeline(ts)
-    got, st = r.trace_tile(u, e, 152, 86, 16, 8, stats=True)  # 16 x 8 px x 8 spp = 1024 paths: one block
+    got, st = r.trace_tile(u, e, 30, 30, 8, 1, stats=True)  # 64 paths: one chunk
     r.sync()  # raises if the launch reported an error
     r.set_wave_timeline(None)
     assert r.scene_info(MM_INFO_LAST_DEFER) == 1.0
@@ -73,9 +93,10 @@ def test_long_chunks_with_tail_rings_end_clean_and_bit_exact(gpu):
     busy = t[t[:, 3] > 0]                              # waves that traced at least one chunk
     span_s = (busy[:, 2] - busy[:, 0]).max() / 100e6   # wall_clock64: 100 MHz
     print(f"longest wave: {span_s:.3f} s; {len(busy)} busy waves, {int(busy[:, 3].sum())} chunks; "
-          f"{st.rays} queries ({st.rays / 1024:.0f} per path)")
+          f"{st.rays} queries ({st.rays / 64:.0f} per path), {st.rect_tests / max(st.rays, 1):.0f} tests each")
+    assert st.rays >= 64 * 32767  # no path escapes the room
     assert span_s > 0.3, span_s
-    ref, rays = oracle_tile(Oracle.from_scene(s), u, e, 152, 86, 16, 8)
+    ref, rays = oracle_tile(Oracle.from_scene(s), u, e, 30, 30, 8, 1)
     assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref))
     assert st.rays == rays
     r.close()
