@@ -21,10 +21,18 @@ constexpr int kStackMax = 50;     // shaders.metal:123
 // kFormGridSlow (internal): the grid search on a scene with SLOW rect records.
 // kFormGridWide / kFormGridWideSlow (internal): the same on a grid with 64-bit
 // cell words (per-face list ranges; grid_build.cpp).
+// kFormGridFlat (internal, + kFormGrid..kFormGridWideSlow): the same on a grid
+// with one cell along y (the walk steps x / z only; mm_grid.h kFlat).
 enum : int {
     kFormIfIf = 0, kFormLeafInterior = 5, kFormLean = 7,
-    kFormGrid = 11, kFormGridSlow = 12, kFormGridWide = 13, kFormGridWideSlow = 14
+    kFormGrid = 11, kFormGridSlow = 12, kFormGridWide = 13, kFormGridWideSlow = 14,
+    kFormGridFlat = 4  // offset: 15..18
 };
+__host__ __device__ constexpr bool grid_form(int f) { return f >= kFormGrid && f <= kFormGridWideSlow + kFormGridFlat; }
+__host__ __device__ constexpr bool grid_flat(int f) { return f > kFormGridWideSlow; }
+__host__ __device__ constexpr int grid_base(int f) { return grid_flat(f) ? f - kFormGridFlat : f; }
+__host__ __device__ constexpr bool grid_slow(int f) { return grid_base(f) == kFormGridSlow || grid_base(f) == kFormGridWideSlow; }
+__host__ __device__ constexpr bool grid_wide(int f) { return grid_base(f) >= kFormGridWide; }
 
 // ---- HBM layouts ------------------------------------------------------------
 // Reference node (nodes_ref): 2 x float4 = the reference's 32-B bvh_node,
@@ -92,8 +100,31 @@ __device__ __forceinline__ float dot3(F3 a, F3 b) {
     s = s + a.y * b.y;
     return s + a.z * b.z;
 }
-// air.fast_rsqrt.f32 -> correctly rounded sqrt, then correctly rounded 1/x
-__device__ __forceinline__ float rsq(float x) { return 1.0f / sqrtf(x); }
+// air.fast_rsqrt.f32 -> correctly rounded sqrt, then correctly rounded 1/x.
+// For x in [2^-40, 2^40] (every normalisation on the path: |x|^2 of a unit-ish
+// vector) the same two roundings come from the hardware sqrt / rcp with exact
+// corrections: the sqrt is LLVM's own correctly rounded expansion without the
+// denormal scaling and the zero / inf class fix-up (x is normal and finite),
+// the reciprocal one fma Newton step on v_rcp_f32; bit-identical to
+// 1.0f / sqrtf(x) for every x in the range (exhaustive GPU check,
+// scripts/verify_fast_rsq.hip, tests/test_gpu_arith.py).  Other x take the
+// IEEE expansion.
+__device__ __forceinline__ float rsq_ieee(float x) { return 1.0f / sqrtf(x); }
+__device__ __forceinline__ float rsq(float x) {
+#ifndef MM_NO_FAST_RSQ
+    if (x >= 0x1p-40f && x <= 0x1p40f) {
+        float s = __builtin_amdgcn_sqrtf(x);
+        const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+        const float vd = __builtin_fmaf(-sd, s, x), vu = __builtin_fmaf(-su, s, x);
+        s = vd <= 0.0f ? sd : s;
+        s = vu > 0.0f ? su : s;
+        const float y = __builtin_amdgcn_rcpf(s);
+        const float e = __builtin_fmaf(-s, y, 1.0f);
+        return __builtin_fmaf(e, y, y);
+    }
+#endif
+    return rsq_ieee(x);
+}
 __device__ __forceinline__ F3 normalize3(F3 v) { return rsq(dot3(v, v)) * v; }
 // cross(v, u) in the IR's operand order (ray_rect_intersect %22-%32)
 __device__ __forceinline__ F3 cross3(F3 v, F3 u) {

@@ -120,6 +120,48 @@ __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restric
     if (hit) grid_update_sel(a, k, best, bk, tie);
 }
 
+// The same test for a record whose normal axis A is known (a global rect:
+// its record is the same for every lane, so the caller branches on its axis
+// uniformly and the per-lane axis selects go away).  v = the lower in-plane
+// axis, u = the higher, as in the record; same operations as grid_rect.
+template <int A>
+__device__ __forceinline__ float ax(F3 v) {
+    return A == 0 ? v.x : (A == 1 ? v.y : v.z);
+}
+template <int A, typename R>
+__device__ __forceinline__ void grid_rect_axis(const R& recs, uint32_t k, const Ray& r, float& best, uint32_t& bk,
+                                               uint32_t& tie) {
+    constexpr int V = A == 0 ? 1 : 0, U = A == 2 ? 1 : 2;
+    const uint4 w0 = recs[2 * k + 0], w1 = recs[2 * k + 1];
+    const float a = qdiv(__uint_as_float(w0.x) - ax<A>(r.o), ax<A>(r.d), ax<A>(r.y));
+    const float y1 = (ax<V>(r.o) - __uint_as_float(w0.y)) + a * ax<V>(r.d);
+    const float y2 = (ax<U>(r.o) - __uint_as_float(w0.z)) + a * ax<U>(r.d);
+    const uint32_t hit = (uint32_t)(y1 >= __uint_as_float(w0.w)) & (uint32_t)(y1 <= __uint_as_float(w1.x)) &
+                         (uint32_t)(y2 >= __uint_as_float(w1.y)) & (uint32_t)(y2 <= __uint_as_float(w1.z)) &
+                         (uint32_t)(a > 0.1f);
+    if (hit) grid_update_sel(a, k, best, bk, tie);
+}
+
+// A global rect (g.glob: the same k for every lane): the record's kind and
+// axis are read once per wave and branched on uniformly.
+template <bool kSlow, typename R>
+__device__ __forceinline__ void grid_rect_uniform(const R& recs, const float4* __restrict__ geo, uint32_t k,
+                                                  const Ray& r, float& best, uint32_t& bk, uint32_t& tie) {
+#ifdef MM_NO_UNIFORM_GLOBALS  // A/B: the per-lane selecting test
+    grid_rect<kSlow>(recs, geo, k, r, best, bk, tie);
+#else
+    const uint32_t meta = __builtin_amdgcn_readfirstlane(recs[2 * k + 1].w);
+    if (kSlow && (meta >> 30) == 2u) {
+        grid_rect_general(geo, k, r, best, bk, tie);
+        return;
+    }
+    const uint32_t ak = (meta >> 20) & 3u;
+    if (ak == 0u) grid_rect_axis<0>(recs, k, r, best, bk, tie);
+    else if (ak == 1u) grid_rect_axis<1>(recs, k, r, best, bk, tie);
+    else grid_rect_axis<2>(recs, k, r, best, bk, tie);
+#endif
+}
+
 // Where the grid's arrays are read from (LDS or global memory).
 template <typename CellsT, typename ListT, typename RecsT, typename BoxT>
 struct GridView {
@@ -165,13 +207,17 @@ __device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, floa
 // Search + certificate.  Returns true with (t, index) = the reference's answer
 // (t = kBig when nothing is hit), false when the caller must walk the BVH.
 // Requires sc.fast_ok && ray_fast_ok(r) && grid_ray_ok.
-template <bool kStats, bool kSlow, bool kWide, typename GV>
+// kFlat: the grid has one cell along y (g.n[1] == 1, grid_build.cpp's merged
+// axis): a y step always leaves the grid, so the walk steps x or z only --
+// the same cells and stop as the general walk, which breaks on the same y
+// step (by leaves 0..n[1]).
+template <bool kStats, bool kSlow, bool kWide, bool kFlat, typename GV>
 __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const float4* __restrict__ geo,
                                             const Ray& r, float& t, uint32_t& index, Counters& c) {
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
     uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
-    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect<kSlow>(gv.recs, geo, g.glob[j], r, best, bk, tie);
+    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect_uniform<kSlow>(gv.recs, geo, g.glob[j], r, best, bk, tie);
     // The walk starts in the cell of the ray's point at t = 3/32, not at the
     // origin: a rect of A has a > 0.1, so the cells the ray occupies only for
     // t < 3/32 hold nothing it can return, and the rounding of the start
@@ -183,7 +229,8 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // further 1.3 % / 1.4 %; bit-identical; profiles/r02_ab_start_cell.txt).
     // The crossing times stay those of the origin.
     const float s0 = 0.09375f;
-    int bx = grid_first(g, 0, r.o.x + s0 * r.d.x, r.y.x), by = grid_first(g, 1, r.o.y + s0 * r.d.y, r.y.y),
+    int bx = grid_first(g, 0, r.o.x + s0 * r.d.x, r.y.x),
+        by = kFlat ? (r.y.y > 0.0f ? 1 : 0) : grid_first(g, 1, r.o.y + s0 * r.d.y, r.y.y),
         bz = grid_first(g, 2, r.o.z + s0 * r.d.z, r.y.z);
     float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
           tz = grid_time(g, 2, bz, r.o.z, r.y.z);
@@ -195,8 +242,9 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // face = 6: the whole list (the first cell).  (A run-time format flag
     // cost 2 % on C3: the format is a template parameter.)
     auto cell_range = [&](uint32_t face, uint32_t& j0, uint32_t& j1) {
-        const int ix = r.y.x > 0.0f ? bx - 1 : bx, iy = r.y.y > 0.0f ? by - 1 : by, iz = r.y.z > 0.0f ? bz - 1 : bz;
-        const uint32_t c = (uint32_t)((iz * g.n[1] + iy) * g.n[0] + ix);
+        const int ix = r.y.x > 0.0f ? bx - 1 : bx, iz = r.y.z > 0.0f ? bz - 1 : bz;
+        const int iy = kFlat ? 0 : (r.y.y > 0.0f ? by - 1 : by);
+        const uint32_t c = kFlat ? (uint32_t)(iz * g.n[0] + ix) : (uint32_t)((iz * g.n[1] + iy) * g.n[0] + ix);
         if constexpr (kWide) {
             const uint64_t cw = reinterpret_cast<const uint64_t*>(gv.cells)[c];
             const bool whole = (cw >> 63) != 0;
@@ -228,6 +276,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             // equal times) -- in selects: three exec-mask branches here cost
             // more SALU and SGPR spills than the selects cost VALU
             const bool sx = tx == te, sy = !sx && ty == te, sz = !sx && !sy;
+            if (kFlat && sy) break;  // (one cell along y: the walk leaves the grid)
             bx += sx ? (r.y.x > 0.0f ? 1 : -1) : 0;
             by += sy ? (r.y.y > 0.0f ? 1 : -1) : 0;
             bz += sz ? (r.y.z > 0.0f ? 1 : -1) : 0;

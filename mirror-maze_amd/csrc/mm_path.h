@@ -31,7 +31,7 @@ struct BvhQuery {
 // global memory (lean loop form, compact records) when the search cannot
 // certify its answer (a tie, a failed leaf-box check) or the ray is outside
 // the Markstein guards or the grid.
-template <bool kStats, bool kSlow, bool kWide, typename GV>
+template <bool kStats, bool kSlow, bool kWide, bool kFlat, typename GV>
 struct GridQuery {
     const DevScene& sc;
     GV gv;
@@ -41,7 +41,7 @@ struct GridQuery {
         bool guards = sc.fast_ok != 0;  // one branch for the three guards
         guards &= ray_fast_ok(r);
         guards &= grid_ray_ok(sc.grid, r);
-        if (guards && grid_search<kStats, kSlow, kWide>(sc.grid, gv, sc.geo, r, t, k, c)) return true;
+        if (guards && grid_search<kStats, kSlow, kWide, kFlat>(sc.grid, gv, sc.geo, r, t, k, c)) return true;
         t = kBig;  // (an out-of-line walk costs 73 VGPR spills of call ABI)
         return closest_hit_bvh<kStats, kSlow ? kFormLeafInterior : kFormLean>(sc, view(sc.nodes, sc.recs), r, t, k,
                                                                               st, c);

@@ -802,14 +802,19 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
         if (!c->grid_ok)
             return fail(c, MM_ERR_UNSUPPORTED, "grid search unavailable for this scene: " + c->grid_why);
         if (!c->lean_ok || c->grid_slow) form = kFormGridSlow;  // general rect tests for the SLOW records
+        // one cell along y: the x / z walk where that form is built (else the general walk, same cells)
+        auto flat = [&](int m) {
+            if (c->grid.n[1] == 1 && wavepersist_built(m, form + kFormGridFlat)) form += kFormGridFlat;
+            mode = m;
+            return MM_OK;
+        };
         if (c->grid_wide) {  // built only when the whole image fits the LDS budget (grid_build.cpp)
             form += kFormGridWide - kFormGrid;
-            mode = c->opt_lds ? 11 : 13;
-            return MM_OK;
+            return flat(c->opt_lds ? 11 : 13);
         }
-        if (c->opt_lds && c->grid.bytes <= budget) { mode = 11; return MM_OK; }
-        if (c->opt_lds && c->grid.off_recs <= budget) { mode = 12; return MM_OK; }
-        if (!auto_form || !c->opt_lds) { mode = 13; return MM_OK; }
+        if (c->opt_lds && c->grid.bytes <= budget) return flat(11);
+        if (c->opt_lds && c->grid.off_recs <= budget) return flat(12);
+        if (!auto_form || !c->opt_lds) return flat(13);
         // the index does not fit LDS: auto takes the BVH (nodes in LDS or cached), which is not
         // measured against the all-global grid
         form = c->lean_ok ? kFormLean : kFormLeafInterior;

@@ -523,7 +523,7 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
                                   reinterpret_cast<const uint16_t*>(index + sc.grid.off_list),
                                   reinterpret_cast<const uint4*>(lds),
                                   reinterpret_cast<const float2*>(base + (sc.grid.off_box - sc.grid.off_recs)));
-        return body(GridQuery<kStats, kForm == kFormGridSlow || kForm == kFormGridWideSlow, kForm >= kFormGridWide, decltype(gv)>{sc, gv});
+        return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 12) {
         const uint32_t n16 = sc.grid.off_recs / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
@@ -534,10 +534,10 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         const auto gv = grid_view(reinterpret_cast<const char*>(base),
                                   reinterpret_cast<const uint16_t*>(base + sc.grid.off_list), sc.grid.recs,
                                   sc.grid.box);
-        return body(GridQuery<kStats, kForm == kFormGridSlow || kForm == kFormGridWideSlow, kForm >= kFormGridWide, decltype(gv)>{sc, gv});
+        return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 13) {
         const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), sc.grid.list, sc.grid.recs, sc.grid.box);
-        return body(GridQuery<kStats, kForm == kFormGridSlow || kForm == kFormGridWideSlow, kForm >= kFormGridWide, decltype(gv)>{sc, gv});
+        return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 6) {
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
         __syncthreads();
@@ -696,11 +696,21 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
 // with global records (7), dictionary nodes (10), loop form 0 -- and the
 // one-thread-per-path kernel are built with `make EXTRA=-DMM_AB_VARIANTS`
 // (mm_version() then ends in "+ab"; every one measured slower).
+// Flat grids (one cell along y) get their own forms where the maze uses them:
+// the whole image in LDS with face ranges (C3) and the index in LDS with plain
+// cells (N=64); other flat placements run the general 3-D walk.
+#ifdef MM_NO_FLAT_GRID
+#define MM_FLAT_INSTANCES(X)
+#else
+#define MM_FLAT_INSTANCES(X)                                                                                  \
+    X(11, kFormGridWide + kFormGridFlat) X(11, kFormGridWideSlow + kFormGridFlat)                             \
+    X(12, kFormGrid + kFormGridFlat) X(12, kFormGridSlow + kFormGridFlat)
+#endif
 #define MM_DEFER_INSTANCES(X)                                                                                 \
     X(11, kFormGrid) X(12, kFormGrid) X(13, kFormGrid)                                                        \
     X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
     X(11, kFormGridWide) X(13, kFormGridWide) X(11, kFormGridWideSlow) X(13, kFormGridWideSlow)               \
-    X(3, kFormLean)
+    MM_FLAT_INSTANCES(X) X(3, kFormLean)
 #ifdef MM_AB_VARIANTS
 #define MM_WP_INSTANCES(X)                                                                                    \
     MM_DEFER_INSTANCES(X) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                    \

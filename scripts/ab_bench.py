@@ -97,8 +97,12 @@ def main():
                 base = out.clone()
             else:
                 same = "bit-identical" if torch.equal(base.view(torch.int32), out.view(torch.int32)) else "MISMATCH"
+            # checksum of the frames' bits, to compare builds (MIRROR_MAZE_LIB) across processes
+            bits = out.view(torch.int32).to(torch.int64)
+            ck = int((bits * torch.arange(1, bits.numel() + 1, device=bits.device).view(bits.shape) % 1000003)
+                     .sum().item())
             print(f"{name:16s} rep {rep} trace {k:8.3f} ms/frame  wall {wall:8.3f} ms/frame  "
-                  f"{st.rays / k / 1e3:9.1f} Mrays/s  launches {kn}  {same}", flush=True)
+                  f"{st.rays / k / 1e3:9.1f} Mrays/s  launches {kn}  {same}  ck {ck:x}", flush=True)
             r.close()
 
 

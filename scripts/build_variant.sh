@@ -13,5 +13,5 @@ if [ "$REV" = wt ]; then
 else
   git -C $ROOT archive $REV include mirror-maze_amd | tar -x -C $D
 fi
-make -s -j8 -C $D/mirror-maze_amd EXTRA="$*" OUT=$D/lib.so BUILD=$D/build
+make -s -j8 -C $D/mirror-maze_amd EXTRA="$*" OUT=$D/lib.so BUILD=$D/build VERIFY=
 echo built $D/lib.so

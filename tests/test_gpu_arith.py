@@ -1,0 +1,28 @@
+"""Exact rewrites of IEEE operations, checked exhaustively on the MI355X.
+
+mm::rsq (mm_device.h) computes the reference's fast_rsqrt with its IEEE
+meaning -- RN(1 / RN(sqrt(x))), the AIR intrinsic as the oracle states it --
+from the hardware v_sqrt_f32 / v_rcp_f32 with exact corrections on
+[2^-40, 2^40].  lib/verify_fast_rsq (scripts/verify_fast_rsq.hip, built by the
+library's Makefile with its flags) compares it with the IEEE expansion
+1.0f / sqrtf(x) for every float x in [2^-44, 2^44]."""
+from __future__ import annotations
+
+import subprocess
+
+import pytest
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fast_rsq_is_bit_identical_to_the_ieee_expansion(gpu):
+    exe = PKG / "lib" / "verify_fast_rsq"
+    assert exe.exists(), "build the library first (make -C mirror-maze_amd)"
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    print(p.stdout)
+    assert p.returncode == 0, p.stdout + p.stderr
+    words = p.stdout.split()
+    checked, bad = int(words[1]), int(words[3])
+    assert checked > 88 * (1 << 23) and bad == 0
