@@ -379,6 +379,13 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     std::vector<uint32_t> grecs;
     g.n_slow = grid_records(recs, n_rects, grecs);
     std::memcpy(&g.image[g.off_recs], grecs.data(), 32u * (size_t)n_rects);
+    // flat forms: one y cell and every listed (non-global) FAST record normal to x or z
+    g.flat_ok = g.n[1] == 1;
+    for (uint32_t k = 0; k < n_rects && g.flat_ok; ++k) {
+        const uint32_t meta = grecs[8 * (size_t)k + 7];
+        const bool global = std::find(g.glob, g.glob + g.n_glob, k) != g.glob + g.n_glob;
+        if (!global && (meta >> 30) == 0u && ((meta >> 20) & 3u) == 1u) g.flat_ok = false;
+    }
     // the reference leaf box of every rect; a rect in no leaf gets an empty
     // box, so a certificate for it always fails (the reference never tests it)
     std::vector<float> box(6 * (size_t)n_rects);

@@ -20,6 +20,9 @@ struct GridHost {
     uint32_t n_list = 0;
     uint32_t n_slow = 0;  // records the kernel tests with the general statement
     bool wide = true;     // 64-bit cell words with face ranges (else 32-bit: first | count << 22)
+    // one cell along y and no listed FAST record with a y normal: the kernel's
+    // flat forms apply (mm_grid.h kFlat: x / z walk, 2-way record selects)
+    bool flat_ok = false;
     std::vector<uint8_t> image;
 };
 

@@ -139,7 +139,13 @@ __device__ __forceinline__ float rand_pm1(uint32_t& state) {
     state = s;
     uint32_t r = ((s >> ((s >> 28) + 4u)) ^ s) * 277803737u;
     r = (r >> 22) ^ r;
+    // RN(RN(float(r) * 2^-31) - 1): the product is exact (a power-of-two
+    // scaling of a float in [1, 2^32]), so one fma rounds the same once
+#ifdef MM_NO_FMA_RAND
     return (float)r * 0x1p-31f - 1.0f;
+#else
+    return __builtin_fmaf((float)r, 0x1p-31f, -1.0f);
+#endif
 }
 
 // air.convert.u.i32.f.f32: truncation, saturating, NaN -> 0

@@ -92,7 +92,10 @@ __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo
 __device__ __forceinline__ float sel_k(bool k0, bool k2, F3 v) { return k0 ? v.x : (k2 ? v.z : v.y); }
 __device__ __forceinline__ float sel_xy(bool sx, bool sy, F3 v) { return sx ? v.x : (sy ? v.y : v.z); }
 
-template <bool kSlow, typename R>
+// kXZ: every listed FAST record has its normal along x or z (the flat grid
+// forms: grid_build.cpp checks it, the maze's y-normal floor and ceiling are
+// global rects), so each select is 2-way.
+template <bool kSlow, bool kXZ = false, typename R>
 __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restrict__ geo, uint32_t k, const Ray& r,
                                           float& best, uint32_t& bk, uint32_t& tie) {
     const uint4 w0 = recs[2 * k + 0], w1 = recs[2 * k + 1];
@@ -104,8 +107,15 @@ __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restric
         }
     }
     const uint32_t ak = (meta >> 20) & 3u;
-    const bool k0 = ak == 0u, k2 = ak == 2u;
-    const float ok = sel_k(k0, k2, r.o), dk = sel_k(k0, k2, r.d), yk = sel_k(k0, k2, r.y);
+#ifdef MM_NO_XZ_SELECT
+    constexpr bool kTwoWay = false;
+#else
+    constexpr bool kTwoWay = kXZ;
+#endif
+    const bool k0 = ak == 0u, k2 = kTwoWay ? !k0 : ak == 2u;
+    const float ok = kTwoWay ? (k0 ? r.o.x : r.o.z) : sel_k(k0, k2, r.o);
+    const float dk = kTwoWay ? (k0 ? r.d.x : r.d.z) : sel_k(k0, k2, r.d);
+    const float yk = kTwoWay ? (k0 ? r.y.x : r.y.z) : sel_k(k0, k2, r.y);
     const float ov = k0 ? r.o.y : r.o.x, dv = k0 ? r.d.y : r.d.x;
     const float ou = k2 ? r.o.y : r.o.z, du = k2 ? r.d.y : r.d.z;
     const float a = qdiv(__uint_as_float(w0.x) - ok, dk, yk);
@@ -210,7 +220,9 @@ __device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, floa
 // kFlat: the grid has one cell along y (g.n[1] == 1, grid_build.cpp's merged
 // axis): a y step always leaves the grid, so the walk steps x or z only --
 // the same cells and stop as the general walk, which breaks on the same y
-// step (by leaves 0..n[1]).
+// step (by leaves 0..n[1]).  The flat forms also need every listed FAST
+// record to have an x or z normal (GridHost::flat_ok), so the list tests use
+// 2-way selects (grid_rect kXZ).
 template <bool kStats, bool kSlow, bool kWide, bool kFlat, typename GV>
 __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const float4* __restrict__ geo,
                                             const Ray& r, float& t, uint32_t& index, Counters& c) {
@@ -265,7 +277,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // is done, step to the next cell (or stop) in the same iteration.
     for (;;) {
         if (j < jend) {
-            grid_rect<kSlow>(gv.recs, geo, (uint32_t)gv.list[j], r, best, bk, tie);
+            grid_rect<kSlow, kFlat>(gv.recs, geo, (uint32_t)gv.list[j], r, best, bk, tie);
             ++j;
             if (kStats) ++tests;
         }

@@ -55,6 +55,7 @@ struct mm_ctx {
     bool grid_ok = false;
     bool grid_slow = false;  // the grid has SLOW records (general rect test)
     bool grid_wide = false;  // 64-bit cell words with per-face list ranges
+    bool grid_flat = false;  // the flat forms apply (grid_build.h GridHost::flat_ok)
     std::string grid_why;
     uint32_t* d_idx = nullptr;
     uint32_t n_rects = 0, n_nodes = 0;
@@ -175,6 +176,7 @@ void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_shade); (void)hipFree(c->d_idx); (void)hipFree(c->d_recs);
     (void)hipFree(c->d_grid);
     c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false; c->grid_slow = false; c->grid_wide = false;
+    c->grid_flat = false;
     (void)hipFree(c->d_dict_tab); (void)hipFree(c->d_dict_words);
     c->d_dict_tab = nullptr; c->d_dict_words = nullptr; c->dict_ok = false;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
@@ -662,6 +664,7 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         dg.off_list = gh.off_list; dg.off_recs = gh.off_recs; dg.off_box = gh.off_box; dg.bytes = gh.bytes;
         c->grid_slow = gh.n_slow > 0;
         c->grid_wide = gh.wide;
+        c->grid_flat = gh.flat_ok;
     }
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     if (dict_ok) {
@@ -804,7 +807,7 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
         if (!c->lean_ok || c->grid_slow) form = kFormGridSlow;  // general rect tests for the SLOW records
         // one cell along y: the x / z walk where that form is built (else the general walk, same cells)
         auto flat = [&](int m) {
-            if (c->grid.n[1] == 1 && wavepersist_built(m, form + kFormGridFlat)) form += kFormGridFlat;
+            if (c->grid_flat && wavepersist_built(m, form + kFormGridFlat)) form += kFormGridFlat;
             mode = m;
             return MM_OK;
         };

@@ -37,14 +37,29 @@ struct Counters {
 
 struct Ray {
     F3 o, d;
-    F3 y;  // (1/d.x, 1/d.y, 1/d.z), IEEE division
+    F3 y;  // (1/d.x, 1/d.y, 1/d.z): RN(1/d) wherever it is read (see make_ray)
 };
+
+// y = RN(1/d) is read only by the Markstein quotients (qdiv) and the grid
+// walk, both only under ray_fast_ok -- |d| in [2^-40, 2^40] on every axis.
+// There one fma Newton step on the hardware v_rcp_f32 gives RN(1/d) exactly
+// (scripts/verify_fast_rsq.hip checks every float of either sign in
+// [2^-44, 2^44]); outside, the value is never used.
+__device__ __forceinline__ float rcp_guarded(float d) {
+#ifdef MM_NO_FAST_RCP
+    return 1.0f / d;
+#else
+    const float y = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, y, 1.0f);
+    return __builtin_fmaf(e, y, y);
+#endif
+}
 
 __device__ __forceinline__ Ray make_ray(F3 o, F3 d) {
     Ray r;
     r.o = o;
     r.d = d;
-    r.y = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    r.y = F3{rcp_guarded(d.x), rcp_guarded(d.y), rcp_guarded(d.z)};
     return r;
 }
 
