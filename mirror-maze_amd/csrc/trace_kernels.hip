@@ -624,9 +624,17 @@ hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s)
 
 // 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
 // 768-thread blocks at 6 waves (80 VGPRs, no VGPR spills) measured 6.21 vs
-// 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).
+// 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).  (A/B builds:
+// -DMM_WP_THREADS=896 -DMM_WP_WAVES=7 and the like.)
+#ifndef MM_WP_THREADS
+#define MM_WP_THREADS 1024
+#endif
+#ifndef MM_WP_WAVES
+#define MM_WP_WAVES 8
+#endif
+constexpr uint32_t kWpThreads = MM_WP_THREADS;
 template <bool kStats, int kLds, int kForm, bool kDefer>
-__global__ __launch_bounds__(1024, 8) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
+__global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {
     if constexpr (kDefer) {  // the block's tail ring: counters and turn words zero
@@ -665,12 +673,12 @@ size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
 template <typename K>
 static uint32_t persistent_grid(K kern, size_t lds, uint32_t reserve_cus, uint64_t items) {
     int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 1024, lds) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kWpThreads, lds) != hipSuccess) return 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int cus_used = std::max(1, cus - (int)reserve_cus);
     uint64_t grid = (uint64_t)std::max(1, per_cu) * (uint64_t)cus_used;
-    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, (items + 1023) / 1024));
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, (items + kWpThreads - 1) / kWpThreads));
 }
 
 template <int kLds, int kForm, bool kDefer>
@@ -684,7 +692,7 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
         persistent_grid(kern, lds, job.reserve_cus, (uint64_t)job.w * job.h * job.e.spp * job.n_frames);
     if (!grid) return hipErrorInvalidValue;
     if (kDefer && (uint64_t)grid * kTailRing > job.tail.cap) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, s, sc, job, samples, stats, err, work);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWpThreads), lds, s, sc, job, samples, stats, err, work);
     return hipGetLastError();
 }
 
