@@ -378,13 +378,46 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     }
     std::vector<uint32_t> grecs;
     g.n_slow = grid_records(recs, n_rects, grecs);
-    std::memcpy(&g.image[g.off_recs], grecs.data(), 32u * (size_t)n_rects);
-    // flat forms: one y cell and every listed (non-global) FAST record normal to x or z
-    g.flat_ok = g.n[1] == 1;
+    // Maze forms: one y cell, no SLOW record, every listed (non-global) record
+    // normal to x or z, and few distinct folded threshold tuples (C3: 22,
+    // N=64: 26 -- the walls come in a handful of lengths and heights)
+    g.flat_ok = g.n[1] == 1 && g.n_slow == 0;
     for (uint32_t k = 0; k < n_rects && g.flat_ok; ++k) {
         const uint32_t meta = grecs[8 * (size_t)k + 7];
         const bool global = std::find(g.glob, g.glob + g.n_glob, k) != g.glob + g.n_glob;
         if (!global && (meta >> 30) == 0u && ((meta >> 20) & 3u) == 1u) g.flat_ok = false;
+    }
+    std::vector<uint32_t> cls;  // 4 words per class
+    std::vector<uint32_t> cls_of(n_rects, 0);
+    for (uint32_t k = 0; k < n_rects && g.flat_ok; ++k) {
+        const uint32_t* t = &grecs[8 * (size_t)k + 3];
+        uint32_t c = 0;
+        while (c < cls.size() / 4 && !std::equal(t, t + 4, &cls[4 * c])) ++c;
+        if (c == cls.size() / 4) {
+            if (c == kMaxClasses) { g.flat_ok = false; break; }
+            cls.insert(cls.end(), t, t + 4);
+        }
+        cls_of[k] = c;
+    }
+    if (g.flat_ok) {
+        // compact records: o_k, o_v, o_u, axis << 20 | class << 24 | kind << 30 (the rect index, implied by
+        // the record's position, is dropped); then the class table; then the leaf boxes
+        g.n_class = (uint32_t)cls.size() / 4;
+        g.off_class = align16(g.off_recs + 16u * n_rects);
+        g.off_box = align16(g.off_class + 16u * kMaxClasses);
+        g.bytes = align16(g.off_box + 24u * n_rects);
+        g.image.resize(g.bytes);
+        std::memset(&g.image[g.off_recs], 0, g.bytes - g.off_recs);
+        for (uint32_t k = 0; k < n_rects; ++k) {
+            const uint32_t* w = &grecs[8 * (size_t)k];
+            const uint32_t meta = (w[7] & (3u << 20)) | (cls_of[k] << 24) | (w[7] & (3u << 30));
+            const uint32_t r[4] = {w[0], w[1], w[2], meta};
+            std::memcpy(&g.image[g.off_recs + 16u * k], r, 16);
+        }
+        std::memcpy(&g.image[g.off_class], cls.data(), 4 * cls.size());
+    } else {
+        g.off_class = 0;
+        std::memcpy(&g.image[g.off_recs], grecs.data(), 32u * (size_t)n_rects);
     }
     // the reference leaf box of every rect; a rect in no leaf gets an empty
     // box, so a certificate for it always fails (the reference never tests it)

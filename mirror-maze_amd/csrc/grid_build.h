@@ -11,6 +11,8 @@
 
 namespace mm {
 
+constexpr uint32_t kMaxClasses = 64;  // threshold classes of compact records (6 bits)
+
 struct GridHost {
     float mn[3], mx[3], cell[3], inv[3];
     int n[3];
@@ -20,9 +22,13 @@ struct GridHost {
     uint32_t n_list = 0;
     uint32_t n_slow = 0;  // records the kernel tests with the general statement
     bool wide = true;     // 64-bit cell words with face ranges (else 32-bit: first | count << 22)
-    // one cell along y and no listed FAST record with a y normal: the kernel's
-    // flat forms apply (mm_grid.h kFlat: x / z walk, 2-way record selects)
+    // The maze forms (mm_grid.h kFlat): one cell along y, every listed record
+    // FAST with an x or z normal, and at most kMaxClasses distinct folded
+    // threshold tuples -- then the records are compact (16 B: origins + meta,
+    // the thresholds in a class table at off_class) and the kernel walks x / z
+    // with 2-way record selects.
     bool flat_ok = false;
+    uint32_t off_class = 0, n_class = 0;
     std::vector<uint8_t> image;
 };
 

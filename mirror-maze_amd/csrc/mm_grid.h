@@ -92,14 +92,52 @@ __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo
 __device__ __forceinline__ float sel_k(bool k0, bool k2, F3 v) { return k0 ? v.x : (k2 ? v.z : v.y); }
 __device__ __forceinline__ float sel_xy(bool sx, bool sy, F3 v) { return sx ? v.x : (sy ? v.y : v.z); }
 
-// kXZ: every listed FAST record has its normal along x or z (the flat grid
-// forms: grid_build.cpp checks it, the maze's y-normal floor and ceiling are
-// global rects), so each select is 2-way.
-template <bool kSlow, bool kXZ = false, typename R>
-__device__ __forceinline__ void grid_rect(const R& recs, const float4* __restrict__ geo, uint32_t k, const Ray& r,
+// Where the grid's arrays are read from (LDS or global memory).
+template <typename CellsT, typename ListT, typename RecsT, typename BoxT, typename ClsT>
+struct GridView {
+    CellsT cells;  // per cell: a 64-bit (wide) or 32-bit word (list range)
+    ListT list;    // rect indices (u16)
+    RecsT recs;    // 2 x uint4 per rect, or 1 (compact records)
+    BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
+    ClsT cls;      // compact records' threshold classes (float4), else unused
+};
+template <typename C, typename L, typename R, typename B, typename K>
+__device__ __forceinline__ GridView<C, L, R, B, K> grid_view(C c, L l, R r, B b, K k) {
+    return GridView<C, L, R, B, K>{c, l, r, b, k};
+}
+
+// Rect k's record: w = (o_k, o_v, o_u, meta) -- meta's axis at bit 20, kind at
+// bit 30 -- and its folded thresholds (Yv_lo, Yv_hi, Yu_lo, Yu_hi).  32-B
+// records hold both; compact records (kCompact, maze grids) hold w and a
+// class index (meta bits 24-29) into the class table.
+template <bool kCompact, typename GV>
+__device__ __forceinline__ uint4 rec_words(const GV& gv, uint32_t k) {
+    if constexpr (kCompact) {
+        return gv.recs[k];
+    } else {
+        const uint4 w0 = gv.recs[2 * k + 0];
+        return make_uint4(w0.x, w0.y, w0.z, gv.recs[2 * k + 1].w);
+    }
+}
+template <bool kCompact, typename GV>
+__device__ __forceinline__ float4 rec_thresholds(const GV& gv, uint32_t k, uint32_t meta) {
+    if constexpr (kCompact) {
+        return gv.cls[(meta >> 24) & 63u];
+    } else {
+        const uint4 w0 = gv.recs[2 * k + 0], w1 = gv.recs[2 * k + 1];
+        return make_float4(__uint_as_float(w0.w), __uint_as_float(w1.x), __uint_as_float(w1.y),
+                           __uint_as_float(w1.z));
+    }
+}
+
+// kXZ: every listed FAST record has its normal along x or z (the maze forms:
+// grid_build.cpp checks it, the maze's y-normal floor and ceiling are global
+// rects), so each select is 2-way.  kCompact: 16-B records + class table.
+template <bool kSlow, bool kXZ, bool kCompact, typename GV>
+__device__ __forceinline__ void grid_rect(const GV& gv, const float4* __restrict__ geo, uint32_t k, const Ray& r,
                                           float& best, uint32_t& bk, uint32_t& tie) {
-    const uint4 w0 = recs[2 * k + 0], w1 = recs[2 * k + 1];
-    const uint32_t meta = w1.w;
+    const uint4 w = rec_words<kCompact>(gv, k);
+    const uint32_t meta = w.w;
     if constexpr (kSlow) {
         if ((meta >> 30) == 2u) {
             grid_rect_general(geo, k, r, best, bk, tie);
@@ -118,15 +156,15 @@ __device__ __forceinline__ void grid_rect(const R& recs, const float4* __restric
     const float yk = kTwoWay ? (k0 ? r.y.x : r.y.z) : sel_k(k0, k2, r.y);
     const float ov = k0 ? r.o.y : r.o.x, dv = k0 ? r.d.y : r.d.x;
     const float ou = k2 ? r.o.y : r.o.z, du = k2 ? r.d.y : r.d.z;
-    const float a = qdiv(__uint_as_float(w0.x) - ok, dk, yk);
-    const float y1 = (ov - __uint_as_float(w0.y)) + a * dv;
-    const float y2 = (ou - __uint_as_float(w0.z)) + a * du;
+    const float4 th = rec_thresholds<kCompact>(gv, k, meta);
+    const float a = qdiv(__uint_as_float(w.x) - ok, dk, yk);
+    const float y1 = (ov - __uint_as_float(w.y)) + a * dv;
+    const float y2 = (ou - __uint_as_float(w.z)) + a * du;
     // One branch around a select-form update (a branch-free update measured
     // 6.11 vs 5.86 ms on C3: most tests miss, and the branch skips the update
     // for the whole wave; && chains compile to one exec-mask branch per clause).
-    const uint32_t hit = (uint32_t)(y1 >= __uint_as_float(w0.w)) & (uint32_t)(y1 <= __uint_as_float(w1.x)) &
-                         (uint32_t)(y2 >= __uint_as_float(w1.y)) & (uint32_t)(y2 <= __uint_as_float(w1.z)) &
-                         (uint32_t)(a > 0.1f);
+    const uint32_t hit = (uint32_t)(y1 >= th.x) & (uint32_t)(y1 <= th.y) & (uint32_t)(y2 >= th.z) &
+                         (uint32_t)(y2 <= th.w) & (uint32_t)(a > 0.1f);
     if (hit) grid_update_sel(a, k, best, bk, tie);
 }
 
@@ -138,51 +176,38 @@ template <int A>
 __device__ __forceinline__ float ax(F3 v) {
     return A == 0 ? v.x : (A == 1 ? v.y : v.z);
 }
-template <int A, typename R>
-__device__ __forceinline__ void grid_rect_axis(const R& recs, uint32_t k, const Ray& r, float& best, uint32_t& bk,
-                                               uint32_t& tie) {
+template <int A, bool kCompact, typename GV>
+__device__ __forceinline__ void grid_rect_axis(const GV& gv, uint32_t k, uint4 w, const Ray& r, float& best,
+                                               uint32_t& bk, uint32_t& tie) {
     constexpr int V = A == 0 ? 1 : 0, U = A == 2 ? 1 : 2;
-    const uint4 w0 = recs[2 * k + 0], w1 = recs[2 * k + 1];
-    const float a = qdiv(__uint_as_float(w0.x) - ax<A>(r.o), ax<A>(r.d), ax<A>(r.y));
-    const float y1 = (ax<V>(r.o) - __uint_as_float(w0.y)) + a * ax<V>(r.d);
-    const float y2 = (ax<U>(r.o) - __uint_as_float(w0.z)) + a * ax<U>(r.d);
-    const uint32_t hit = (uint32_t)(y1 >= __uint_as_float(w0.w)) & (uint32_t)(y1 <= __uint_as_float(w1.x)) &
-                         (uint32_t)(y2 >= __uint_as_float(w1.y)) & (uint32_t)(y2 <= __uint_as_float(w1.z)) &
-                         (uint32_t)(a > 0.1f);
+    const float4 th = rec_thresholds<kCompact>(gv, k, w.w);
+    const float a = qdiv(__uint_as_float(w.x) - ax<A>(r.o), ax<A>(r.d), ax<A>(r.y));
+    const float y1 = (ax<V>(r.o) - __uint_as_float(w.y)) + a * ax<V>(r.d);
+    const float y2 = (ax<U>(r.o) - __uint_as_float(w.z)) + a * ax<U>(r.d);
+    const uint32_t hit = (uint32_t)(y1 >= th.x) & (uint32_t)(y1 <= th.y) & (uint32_t)(y2 >= th.z) &
+                         (uint32_t)(y2 <= th.w) & (uint32_t)(a > 0.1f);
     if (hit) grid_update_sel(a, k, best, bk, tie);
 }
 
 // A global rect (g.glob: the same k for every lane): the record's kind and
 // axis are read once per wave and branched on uniformly.
-template <bool kSlow, typename R>
-__device__ __forceinline__ void grid_rect_uniform(const R& recs, const float4* __restrict__ geo, uint32_t k,
+template <bool kSlow, bool kCompact, typename GV>
+__device__ __forceinline__ void grid_rect_uniform(const GV& gv, const float4* __restrict__ geo, uint32_t k,
                                                   const Ray& r, float& best, uint32_t& bk, uint32_t& tie) {
 #ifdef MM_NO_UNIFORM_GLOBALS  // A/B: the per-lane selecting test
-    grid_rect<kSlow>(recs, geo, k, r, best, bk, tie);
+    grid_rect<kSlow, false, kCompact>(gv, geo, k, r, best, bk, tie);
 #else
-    const uint32_t meta = __builtin_amdgcn_readfirstlane(recs[2 * k + 1].w);
+    const uint4 w = rec_words<kCompact>(gv, k);
+    const uint32_t meta = __builtin_amdgcn_readfirstlane(w.w);
     if (kSlow && (meta >> 30) == 2u) {
         grid_rect_general(geo, k, r, best, bk, tie);
         return;
     }
     const uint32_t ak = (meta >> 20) & 3u;
-    if (ak == 0u) grid_rect_axis<0>(recs, k, r, best, bk, tie);
-    else if (ak == 1u) grid_rect_axis<1>(recs, k, r, best, bk, tie);
-    else grid_rect_axis<2>(recs, k, r, best, bk, tie);
+    if (ak == 0u) grid_rect_axis<0, kCompact>(gv, k, w, r, best, bk, tie);
+    else if (ak == 1u) grid_rect_axis<1, kCompact>(gv, k, w, r, best, bk, tie);
+    else grid_rect_axis<2, kCompact>(gv, k, w, r, best, bk, tie);
 #endif
-}
-
-// Where the grid's arrays are read from (LDS or global memory).
-template <typename CellsT, typename ListT, typename RecsT, typename BoxT>
-struct GridView {
-    CellsT cells;  // per cell: a 64-bit (wide) or 32-bit word (list range)
-    ListT list;    // rect indices (u16)
-    RecsT recs;    // 2 x uint4 per rect
-    BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
-};
-template <typename C, typename L, typename R, typename B>
-__device__ __forceinline__ GridView<C, L, R, B> grid_view(C c, L l, R r, B b) {
-    return GridView<C, L, R, B>{c, l, r, b};
 }
 
 // (&=, not &&: see ray_fast_ok)
@@ -220,16 +245,16 @@ __device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, floa
 // kFlat: the grid has one cell along y (g.n[1] == 1, grid_build.cpp's merged
 // axis): a y step always leaves the grid, so the walk steps x or z only --
 // the same cells and stop as the general walk, which breaks on the same y
-// step (by leaves 0..n[1]).  The flat forms also need every listed FAST
-// record to have an x or z normal (GridHost::flat_ok), so the list tests use
-// 2-way selects (grid_rect kXZ).
+// step (by leaves 0..n[1]).  These "maze forms" also need every listed record
+// FAST with an x or z normal and read compact records (GridHost::flat_ok), so
+// the list tests use 2-way selects and one 16-B record + a class-table entry.
 template <bool kStats, bool kSlow, bool kWide, bool kFlat, typename GV>
 __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, const float4* __restrict__ geo,
                                             const Ray& r, float& t, uint32_t& index, Counters& c) {
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
     uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
-    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect_uniform<kSlow>(gv.recs, geo, g.glob[j], r, best, bk, tie);
+    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
     // The walk starts in the cell of the ray's point at t = 3/32, not at the
     // origin: a rect of A has a > 0.1, so the cells the ray occupies only for
     // t < 3/32 hold nothing it can return, and the rounding of the start
@@ -277,7 +302,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // is done, step to the next cell (or stop) in the same iteration.
     for (;;) {
         if (j < jend) {
-            grid_rect<kSlow, kFlat>(gv.recs, geo, (uint32_t)gv.list[j], r, best, bk, tie);
+            grid_rect<kSlow, kFlat, kFlat>(gv, geo, (uint32_t)gv.list[j], r, best, bk, tie);
             ++j;
             if (kStats) ++tests;
         }

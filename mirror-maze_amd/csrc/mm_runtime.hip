@@ -662,6 +662,8 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         dg.box = reinterpret_cast<const float2*>(c->d_grid + gh.off_box);
         dg.image = reinterpret_cast<const uint4*>(c->d_grid);
         dg.off_list = gh.off_list; dg.off_recs = gh.off_recs; dg.off_box = gh.off_box; dg.bytes = gh.bytes;
+        dg.off_class = gh.off_class;  // 0: 32-byte records, no class table
+        dg.cls = gh.off_class ? reinterpret_cast<const float4*>(c->d_grid + gh.off_class) : nullptr;
         c->grid_slow = gh.n_slow > 0;
         c->grid_wide = gh.wide;
         c->grid_flat = gh.flat_ok;
@@ -805,9 +807,16 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
         if (!c->grid_ok)
             return fail(c, MM_ERR_UNSUPPORTED, "grid search unavailable for this scene: " + c->grid_why);
         if (!c->lean_ok || c->grid_slow) form = kFormGridSlow;  // general rect tests for the SLOW records
-        // one cell along y: the x / z walk where that form is built (else the general walk, same cells)
+        // maze grids (one cell along y, compact records): only the maze forms read them
         auto flat = [&](int m) {
-            if (c->grid_flat && wavepersist_built(m, form + kFormGridFlat)) form += kFormGridFlat;
+            if (c->grid_flat) {
+                if (form != kFormGrid && form != kFormGridWide)
+                    return fail(c, MM_ERR_UNSUPPORTED, "maze grid with SLOW records");
+                form += kFormGridFlat;
+            }
+            if (!wavepersist_built(m, form))
+                return fail(c, MM_ERR_UNSUPPORTED,
+                            "grid form " + std::to_string(form) + " not built for LDS mode " + std::to_string(m));
             mode = m;
             return MM_OK;
         };
@@ -816,6 +825,8 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
             return flat(c->opt_lds ? 11 : 13);
         }
         if (c->opt_lds && c->grid.bytes <= budget) return flat(11);
+        // compact records + class table + index (N=64: ~77 KB), leaf boxes global
+        if (c->opt_lds && c->grid_flat && c->grid.off_box <= budget) return flat(14);
         if (c->opt_lds && c->grid.off_recs <= budget) return flat(12);
         if (!auto_form || !c->opt_lds) return flat(13);
         // the index does not fit LDS: auto takes the BVH (nodes in LDS or cached), which is not

@@ -495,6 +495,8 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
 //   11 the whole grid image                       grid search
 //   12 grid cells + lists, records + boxes global grid search
 //   13 nothing (the grid image global)             grid search
+//   14 grid records + class table + cells + lists, grid search (compact records: the maze forms)
+//      leaf boxes global
 // stage_and_run fills the block's LDS for the mode and calls body(query).
 template <int kLds, int kForm, bool kStats, typename F>
 __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const TileJob& job, F&& body) {
@@ -507,10 +509,11 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
 #endif
         }
     };
-    if constexpr (kLds == 11) {
-        // records + boxes first, at LDS address 0 (a constant in the rect test),
-        // then cells + lists
-        const uint32_t nr16 = (sc.grid.bytes - sc.grid.off_recs) / 16u, ni16 = sc.grid.off_recs / 16u;
+    if constexpr (kLds == 11 || kLds == 14) {
+        // records (+ class table) (+ boxes: mode 11) first, at LDS address 0 (a
+        // constant in the rect test), then cells + lists
+        const uint32_t end = kLds == 11 ? sc.grid.bytes : sc.grid.off_box;
+        const uint32_t nr16 = (end - sc.grid.off_recs) / 16u, ni16 = sc.grid.off_recs / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
         const uint4* src = sc.grid.image;
         for (uint32_t i = threadIdx.x; i < nr16; i += blockDim.x) img[i] = src[ni16 + i];
@@ -519,11 +522,17 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         staged();
         const char* base = reinterpret_cast<const char*>(lds);
         const char* index = base + 16u * nr16;
-        const auto gv = grid_view(reinterpret_cast<const char*>(index),
-                                  reinterpret_cast<const uint16_t*>(index + sc.grid.off_list),
-                                  reinterpret_cast<const uint4*>(lds),
-                                  reinterpret_cast<const float2*>(base + (sc.grid.off_box - sc.grid.off_recs)));
-        return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
+        const auto cls = reinterpret_cast<const float4*>(base + (sc.grid.off_class - sc.grid.off_recs));
+        const auto run = [&](auto box) {
+            const auto gv = grid_view(reinterpret_cast<const char*>(index),
+                                      reinterpret_cast<const uint16_t*>(index + sc.grid.off_list),
+                                      reinterpret_cast<const uint4*>(lds), box, cls);
+            return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
+        };
+        if constexpr (kLds == 11)
+            return run(reinterpret_cast<const float2*>(base + (sc.grid.off_box - sc.grid.off_recs)));
+        else
+            return run(sc.grid.box);
     } else if constexpr (kLds == 12) {
         const uint32_t n16 = sc.grid.off_recs / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
@@ -533,10 +542,11 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         const char* base = reinterpret_cast<const char*>(lds);
         const auto gv = grid_view(reinterpret_cast<const char*>(base),
                                   reinterpret_cast<const uint16_t*>(base + sc.grid.off_list), sc.grid.recs,
-                                  sc.grid.box);
+                                  sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 13) {
-        const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), sc.grid.list, sc.grid.recs, sc.grid.box);
+        const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), sc.grid.list, sc.grid.recs,
+                                  sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 6) {
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
@@ -660,6 +670,7 @@ size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
     switch (lds_mode) {
         case 11: return sc.grid.bytes;
         case 12: return sc.grid.off_recs;
+        case 14: return sc.grid.off_box;
         case 6: return (size_t)sc.n_lds_f4 * sizeof(float4);
         case 10: return 256 * sizeof(float) + 3 * (size_t)sc.n_nodes * sizeof(uint32_t);
         case 1: case 7: return 2 * (size_t)sc.n_nodes * sizeof(float4);
@@ -704,16 +715,12 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
 // with global records (7), dictionary nodes (10), loop form 0 -- and the
 // one-thread-per-path kernel are built with `make EXTRA=-DMM_AB_VARIANTS`
 // (mm_version() then ends in "+ab"; every one measured slower).
-// Flat grids (one cell along y) get their own forms where the maze uses them:
-// the whole image in LDS with face ranges (C3) and the index in LDS with plain
-// cells (N=64); other flat placements run the general 3-D walk.
-#ifdef MM_NO_FLAT_GRID
-#define MM_FLAT_INSTANCES(X)
-#else
+// The maze forms (flat grid walk, compact records; grid_build.cpp decides)
+// in every grid placement: a maze grid's compact records are read by no other
+// form.  (No SLOW records in maze grids: no slow maze forms.)
 #define MM_FLAT_INSTANCES(X)                                                                                  \
-    X(11, kFormGridWide + kFormGridFlat) X(11, kFormGridWideSlow + kFormGridFlat)                             \
-    X(12, kFormGrid + kFormGridFlat) X(12, kFormGridSlow + kFormGridFlat)
-#endif
+    X(11, kFormGridWide + kFormGridFlat) X(11, kFormGrid + kFormGridFlat) X(14, kFormGrid + kFormGridFlat)     \
+    X(12, kFormGrid + kFormGridFlat) X(13, kFormGridWide + kFormGridFlat) X(13, kFormGrid + kFormGridFlat)
 #define MM_DEFER_INSTANCES(X)                                                                                 \
     X(11, kFormGrid) X(12, kFormGrid) X(13, kFormGrid)                                                        \
     X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
