@@ -16,6 +16,32 @@ namespace mm {
 constexpr float kBig = 1e30f;     // shaders.metal:15, 94, 149 (IR 0x46293E5940000000)
 constexpr int kStackMax = 50;     // shaders.metal:123
 
+// Diagnostics build (-DMM_LANE_STATS, scripts/lane_probe.py): per phase of the
+// bounce loop, the wave-iterations that run it and the lanes active in them,
+// counted in block-local LDS words and added to the wave-timeline buffer at
+// exit.  Not a product build: the counting perturbs the timing.
+enum LanePhase : int {
+    kLpChunk, kLpBounce, kLpGlobal, kLpGridIter, kLpRectTest, kLpCellStep, kLpCert, kLpFallback,
+    kLpShade, kLpDiffuse, kLpTrial, kLpMirror, kLpCount
+};
+constexpr uint32_t kLaneStatRecord = 49152;  // wave-timeline record (4 x u64) where the totals start
+#ifdef MM_LANE_STATS
+__device__ __forceinline__ uint32_t* lane_stat_words() {
+    __shared__ uint32_t words[2 * kLpCount];
+    return words;
+}
+__device__ __forceinline__ void lane_stat(int ph) {
+    const uint64_t m = __ballot(1);
+    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)m) - 1)) {
+        atomicAdd(lane_stat_words() + 2 * ph, 1u);
+        atomicAdd(lane_stat_words() + 2 * ph + 1, (uint32_t)__popcll(m));
+    }
+}
+#define MM_LANE_STAT(ph) ::mm::lane_stat(::mm::ph)
+#else
+#define MM_LANE_STAT(ph) ((void)0)
+#endif
+
 // Closest-hit query methods of the wave-persistent kernel (MM_OPT_TRAVERSAL):
 // BVH loop forms (mm_trace.h) and the certified grid search (mm_grid.h).
 // kFormGridSlow (internal): the grid search on a scene with SLOW rect records.

@@ -254,7 +254,10 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
     uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
-    for (uint32_t j = 0; j < g.n_glob; ++j) grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
+    for (uint32_t j = 0; j < g.n_glob; ++j) {
+        MM_LANE_STAT(kLpGlobal);
+        grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
+    }
     // The walk starts in the cell of the ray's point at t = 3/32, not at the
     // origin: a rect of A has a > 0.1, so the cells the ray occupies only for
     // t < 3/32 hold nothing it can return, and the rounding of the start
@@ -301,12 +304,15 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // One iteration: test one rect of the current cell; when the cell's list
     // is done, step to the next cell (or stop) in the same iteration.
     for (;;) {
+        MM_LANE_STAT(kLpGridIter);
         if (j < jend) {
+            MM_LANE_STAT(kLpRectTest);
             grid_rect<kSlow, kFlat, kFlat>(gv, geo, (uint32_t)gv.list[j], r, best, bk, tie);
             ++j;
             if (kStats) ++tests;
         }
         if (j >= jend) {
+            MM_LANE_STAT(kLpCellStep);
             const float te = fminf(tx, fminf(ty, tz));
             if (best < te) break;
             // step the axis whose boundary comes first (x before y before z on
@@ -344,6 +350,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         return !tie;
     }
     if (tie) return false;
+    MM_LANE_STAT(kLpCert);
     // certificate: R*'s reference leaf box passes at every t > best
     const float2 bxx = gv.box[3 * bk + 0], byy = gv.box[3 * bk + 1], bzz = gv.box[3 * bk + 2];
     const float tx1 = qdiv(bxx.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(bxx.y - r.o.x, r.d.x, r.y.x);

@@ -42,6 +42,7 @@ struct GridQuery {
         guards &= ray_fast_ok(r);
         guards &= grid_ray_ok(sc.grid, r);
         if (guards && grid_search<kStats, kSlow, kWide, kFlat>(sc.grid, gv, sc.geo, r, t, k, c)) return true;
+        MM_LANE_STAT(kLpFallback);
         t = kBig;  // (an out-of-line walk costs 73 VGPR spills of call ABI)
         return closest_hit_bvh<kStats, kSlow ? kFormLeafInterior : kFormLean>(sc, view(sc.nodes, sc.recs), r, t, k,
                                                                               st, c);
@@ -60,6 +61,7 @@ __device__ __forceinline__ bool bounce_loop_r(const DevScene& sc, const Q& query
                                               int defer_from, uint32_t defer_lanes, Reserve&& reserve) {
     for (; p.n < bounce_limit + p.mh; ++p.n) {
         if (p.n >= defer_from && (uint32_t)__popcll(__ballot(1)) <= defer_lanes && reserve()) return true;
+        MM_LANE_STAT(kLpBounce);
         float t = kBig;
         uint32_t k = 0;
 #ifdef MM_PHASE_CLOCKS

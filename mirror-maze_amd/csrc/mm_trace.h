@@ -482,6 +482,7 @@ struct PathState {
 // after line 307).  Returns false when the path terminates.
 __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, float t, uint32_t k, int mirror_limit) {
     if (!(t < kBig)) return false;                           // miss, shaders.metal:336-338
+    MM_LANE_STAT(kLpShade);
     const F3 nn = xyz(sc.geo[4 * k + 1]);                    // normalize(cross(v,u)), %238
     const float4 s0 = sc.shade[2 * k + 0];                   // color, is_mirror
     const float sg = msign(dot3(p.dir, nn));
@@ -492,6 +493,7 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
     // would otherwise execute the correctly rounded 1/sqrt of each branch).
     F3 x, contrib;
     if (diffuse) {
+        MM_LANE_STAT(kLpDiffuse);
         const float side = -sg;
         const float4 e = sc.shade[2 * k + 1];
         contrib = (e.w * p.T) * xyz(e);                      // %253, %254
@@ -505,6 +507,7 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         // over the others with jumps of the random() state -- was bit-exact and
         // 12 % slower on C3, profiles/r02_ab_grid_salu.txt)
         while (len2 > 0x1.000002p0f) {
+            MM_LANE_STAT(kLpTrial);
             rx = rand_pm1(p.seed); ry = rand_pm1(p.seed); rz = rand_pm1(p.seed);
             rd = F3{rx, ry, rz};
             len2 = dot3(rd, rd);
@@ -512,6 +515,7 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         const F3 rn = rsq(len2) * rd;                        // %358
         x = rn + side * nn;                                  // %367
     } else {
+        MM_LANE_STAT(kLpMirror);
         contrib = 0.005f * xyz(s0);                          // %386
         const float dd = dot3(nn, p.dir) * 2.0f;             // reflect, %392-%397
         x = p.dir - dd * nn;

@@ -442,6 +442,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             }
         }
         if (live) {
+            MM_LANE_STAT(kLpChunk);
             bool overflow = false;
             uint32_t seq = 0;
             const bool deferred = bounce_loop_r<kStats>(
@@ -652,6 +653,10 @@ __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersis
         __syncthreads();
     }
     if (job.fault == 1u && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, kErrInjected);
+#ifdef MM_LANE_STATS
+    if (threadIdx.x < 2u * kLpCount) lane_stat_words()[threadIdx.x] = 0u;
+    __syncthreads();
+#endif
 #ifdef MM_PHASE_CLOCKS
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
 #else
@@ -663,6 +668,12 @@ __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersis
         else
             return wavepersist_body<kStats>(sc, q, job, samples, stats, err, work);
     });
+#ifdef MM_LANE_STATS
+    __syncthreads();  // every wave of the block is done: add its counts to the timeline buffer
+    if (job.wave_ts && job.wave_ts_cap >= kLaneStatRecord + (2u * kLpCount + 3u) / 4u &&
+        threadIdx.x < 2u * kLpCount)
+        atomicAdd(job.wave_ts + 4u * kLaneStatRecord + threadIdx.x, (unsigned long long)lane_stat_words()[threadIdx.x]);
+#endif
     persistent_exit(job, chunks, t_entry, work, err);
 }
 
