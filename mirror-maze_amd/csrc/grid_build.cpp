@@ -338,7 +338,8 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
 // extent and grows by 1.25x until the cells + lists (the part the kernel keeps
 // in LDS) fit index_budget bytes.
 bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
-                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why, bool merge_axes) {
+                const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why, bool merge_axes,
+                double cell_scale) {
     if (n_rects == 0 || n_rects > 65535) { why = "rect count outside 1..65535"; return false; }
     std::vector<uint32_t> ident(n_rects), recs;
     for (uint32_t k = 0; k < n_rects; ++k) ident[k] = k;
@@ -363,49 +364,60 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     }
     if (ext2.empty()) { why = "no rect with area"; return false; }
     std::nth_element(ext2.begin(), ext2.begin() + ext2.size() / 2, ext2.end());
-    double s = ext2[ext2.size() / 2];
+    // grid records and their threshold classes do not depend on the cells
+    std::vector<uint32_t> grecs;
+    const uint32_t n_slow_g = grid_records(recs, n_rects, grecs);
+    std::vector<uint32_t> cls;  // 4 words per class
+    std::vector<uint32_t> cls_of(n_rects, 0);
+    bool classes_ok = n_slow_g == 0;
+    for (uint32_t k = 0; k < n_rects && classes_ok; ++k) {
+        const uint32_t* t = &grecs[8 * (size_t)k + 3];
+        uint32_t c = 0;
+        while (c < cls.size() / 4 && !std::equal(t, t + 4, &cls[4 * c])) ++c;
+        if (c == cls.size() / 4) {
+            if (c == kMaxClasses) { classes_ok = false; break; }
+            cls.insert(cls.end(), t, t + 4);
+        }
+        cls_of[k] = c;
+    }
+    // Maze forms: one y cell, no SLOW record, every listed (non-global) record
+    // normal to x or z, and few distinct folded threshold tuples (C3: 22,
+    // N=64: 26 -- the walls come in a handful of lengths and heights)
+    auto maze_form = [&](const GridHost& gg) {
+        if (gg.n[1] != 1 || !classes_ok) return false;
+        for (uint32_t k = 0; k < n_rects; ++k) {
+            const uint32_t meta = grecs[8 * (size_t)k + 7];
+            const bool global = std::find(gg.glob, gg.glob + gg.n_glob, k) != gg.glob + gg.n_glob;
+            if (!global && (meta >> 30) == 0u && ((meta >> 20) & 3u) == 1u) return false;
+        }
+        return true;
+    };
+    // compact records: o_k, o_v, o_u, axis << 20 | class << 24 | kind << 30 (the rect index, implied by
+    // the record's position, is dropped); then the class table; then the leaf boxes
+    auto compact_layout = [&](GridHost& gg) {
+        gg.off_class = align16(gg.off_recs + 16u * n_rects);
+        gg.off_box = align16(gg.off_class + 16u * kMaxClasses);
+        gg.bytes = align16(gg.off_box + 24u * n_rects);
+    };
+    double s = ext2[ext2.size() / 2] * cell_scale;
     for (int attempt = 0; attempt < 24; ++attempt, s *= 1.25) {
         // 64-bit cell words with face ranges where the whole image fits the
         // budget, else plain 32-bit words at the same cell size, before
         // coarser cells (the kernel variant for wide words stages all of it)
-        if (build_lists(rects, n_rects, recs, smin, smax, C, s, true, merge_axes, g, why) &&
-            g.bytes <= index_budget)
-            break;
+        if (build_lists(rects, n_rects, recs, smin, smax, C, s, true, merge_axes, g, why)) {
+            if (maze_form(g)) compact_layout(g);
+            if (g.bytes <= index_budget) break;
+        }
         if (build_lists(rects, n_rects, recs, smin, smax, C, s, false, merge_axes, g, why) &&
             g.off_recs <= index_budget)
             break;
         if (attempt == 23) { why = "no grid index fits the LDS budget"; return false; }
     }
-    std::vector<uint32_t> grecs;
-    g.n_slow = grid_records(recs, n_rects, grecs);
-    // Maze forms: one y cell, no SLOW record, every listed (non-global) record
-    // normal to x or z, and few distinct folded threshold tuples (C3: 22,
-    // N=64: 26 -- the walls come in a handful of lengths and heights)
-    g.flat_ok = g.n[1] == 1 && g.n_slow == 0;
-    for (uint32_t k = 0; k < n_rects && g.flat_ok; ++k) {
-        const uint32_t meta = grecs[8 * (size_t)k + 7];
-        const bool global = std::find(g.glob, g.glob + g.n_glob, k) != g.glob + g.n_glob;
-        if (!global && (meta >> 30) == 0u && ((meta >> 20) & 3u) == 1u) g.flat_ok = false;
-    }
-    std::vector<uint32_t> cls;  // 4 words per class
-    std::vector<uint32_t> cls_of(n_rects, 0);
-    for (uint32_t k = 0; k < n_rects && g.flat_ok; ++k) {
-        const uint32_t* t = &grecs[8 * (size_t)k + 3];
-        uint32_t c = 0;
-        while (c < cls.size() / 4 && !std::equal(t, t + 4, &cls[4 * c])) ++c;
-        if (c == cls.size() / 4) {
-            if (c == kMaxClasses) { g.flat_ok = false; break; }
-            cls.insert(cls.end(), t, t + 4);
-        }
-        cls_of[k] = c;
-    }
+    g.n_slow = n_slow_g;
+    g.flat_ok = maze_form(g);
     if (g.flat_ok) {
-        // compact records: o_k, o_v, o_u, axis << 20 | class << 24 | kind << 30 (the rect index, implied by
-        // the record's position, is dropped); then the class table; then the leaf boxes
         g.n_class = (uint32_t)cls.size() / 4;
-        g.off_class = align16(g.off_recs + 16u * n_rects);
-        g.off_box = align16(g.off_class + 16u * kMaxClasses);
-        g.bytes = align16(g.off_box + 24u * n_rects);
+        compact_layout(g);
         g.image.resize(g.bytes);
         std::memset(&g.image[g.off_recs], 0, g.bytes - g.off_recs);
         for (uint32_t k = 0; k < n_rects; ++k) {
@@ -417,6 +429,9 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         std::memcpy(&g.image[g.off_class], cls.data(), 4 * cls.size());
     } else {
         g.off_class = 0;
+        g.off_box = align16(g.off_recs + 32u * n_rects);
+        g.bytes = align16(g.off_box + 24u * n_rects);
+        g.image.resize(g.bytes);
         std::memcpy(&g.image[g.off_recs], grecs.data(), 32u * (size_t)n_rects);
     }
     // the reference leaf box of every rect; a rect in no leaf gets an empty

@@ -43,6 +43,8 @@ VARIANTS = {
     "defer-min0": (1, {22: 0}),     # deferral on launches of any size
     "wave": (2, {}),
     "ref": (3, {}),
+    "cell60": (1, {25: 60}), "cell70": (1, {25: 70}), "cell80": (1, {25: 80}), "cell90": (1, {25: 90}),
+    "cell110": (1, {25: 110}), "cell125": (1, {25: 125}), "cell140": (1, {25: 140}), "cell160": (1, {25: 160}),
     "nomerge": (1, {24: 0}),        # MM_OPT_GRID_MERGE 0: cells along y by the rect size (round 2's grid)
     "grid-global-nomerge": (1, {1: 0, 24: 0}),
 }
@@ -101,8 +103,11 @@ def main():
             bits = out.view(torch.int32).to(torch.int64)
             ck = int((bits * torch.arange(1, bits.numel() + 1, device=bits.device).view(bits.shape) % 1000003)
                      .sum().item())
+            gi = "grid %dx%dx%d %s %.0fKB lds%d" % (
+                r.scene_info(2), r.scene_info(3), r.scene_info(4), "faces" if r.scene_info(13) else "plain",
+                r.scene_info(6) / 1024, r.scene_info(12)) if r.scene_info(1) else "no grid"
             print(f"{name:16s} rep {rep} trace {k:8.3f} ms/frame  wall {wall:8.3f} ms/frame  "
-                  f"{st.rays / k / 1e3:9.1f} Mrays/s  launches {kn}  {same}  ck {ck:x}", flush=True)
+                  f"{st.rays / k / 1e3:9.1f} Mrays/s  launches {kn}  {same}  ck {ck:x}  {gi}", flush=True)
             r.close()
 
 
