@@ -370,8 +370,15 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     std::vector<uint32_t> cls;  // 4 words per class
     std::vector<uint32_t> cls_of(n_rects, 0);
     bool classes_ok = n_slow_g == 0;
+    // compact (maze) records keep y as the first in-plane axis: a z-normal
+    // record's (v, u) = (x, y) is stored as (y, x) -- its o_v / o_u and its
+    // threshold pairs swapped -- so the kernel reads y for the first in-plane
+    // axis of every listed record without a select (mm_grid.h grid_rect)
+    auto y_first = [&](uint32_t k) { return ((grecs[8 * (size_t)k + 7] >> 20) & 3u) == 2u; };
     for (uint32_t k = 0; k < n_rects && classes_ok; ++k) {
-        const uint32_t* t = &grecs[8 * (size_t)k + 3];
+        const uint32_t* g8 = &grecs[8 * (size_t)k + 3];
+        uint32_t t[4] = {g8[0], g8[1], g8[2], g8[3]};
+        if (y_first(k)) { std::swap(t[0], t[2]); std::swap(t[1], t[3]); }
         uint32_t c = 0;
         while (c < cls.size() / 4 && !std::equal(t, t + 4, &cls[4 * c])) ++c;
         if (c == cls.size() / 4) {
@@ -392,8 +399,9 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         }
         return true;
     };
-    // compact records: o_k, o_v, o_u, axis << 20 | class << 24 | kind << 30 (the rect index, implied by
-    // the record's position, is dropped); then the class table; then the leaf boxes
+    // compact records: o_k, o_v, o_u (y first, above), class << 4 | axis << 20 | kind << 30 (the rect index,
+    // implied by the record's position, is dropped; the class's byte offset in the table is meta & 0x3F0,
+    // and a listed record's axis is x iff meta < 2^20); then the class table; then the leaf boxes
     auto compact_layout = [&](GridHost& gg) {
         gg.off_class = align16(gg.off_recs + 16u * n_rects);
         gg.off_box = align16(gg.off_class + 16u * kMaxClasses);
@@ -422,8 +430,8 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         std::memset(&g.image[g.off_recs], 0, g.bytes - g.off_recs);
         for (uint32_t k = 0; k < n_rects; ++k) {
             const uint32_t* w = &grecs[8 * (size_t)k];
-            const uint32_t meta = (w[7] & (3u << 20)) | (cls_of[k] << 24) | (w[7] & (3u << 30));
-            const uint32_t r[4] = {w[0], w[1], w[2], meta};
+            const uint32_t meta = (w[7] & (3u << 20)) | (cls_of[k] << 4) | (w[7] & (3u << 30));
+            const uint32_t r[4] = {w[0], y_first(k) ? w[2] : w[1], y_first(k) ? w[1] : w[2], meta};
             std::memcpy(&g.image[g.off_recs + 16u * k], r, 16);
         }
         std::memcpy(&g.image[g.off_class], cls.data(), 4 * cls.size());

@@ -25,8 +25,9 @@
 // current cell (or the ray leaves the grid).  Every rect of A with a <= the
 // final best is tested: its hit point P = o + a d lies within
 // delta ~ 10 u C of the rect (the rounding of the reference's bounds test,
-// u = 2^-24), and the computed crossing times put the ray at any
-// t <= (the last exit time) within eta ~ 5 u C of a visited cell, so the
+// u = 2^-24), and the computed crossing times (one fma per step, see
+// grid_search) put the ray at any t <= (the last exit time) within
+// eta ~ 8 u C of a visited cell, so the
 // rect comes within delta + eta << eps of a visited cell and is on its list.
 // The exact per-rect operations (the compact records of rect_compact.cpp)
 // give each rect's a, so the minimum and whether it is attained twice are
@@ -122,7 +123,7 @@ __device__ __forceinline__ uint4 rec_words(const GV& gv, uint32_t k) {
 template <bool kCompact, typename GV>
 __device__ __forceinline__ float4 rec_thresholds(const GV& gv, uint32_t k, uint32_t meta) {
     if constexpr (kCompact) {
-        return gv.cls[(meta >> 24) & 63u];
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(gv.cls) + (meta & 0x3F0u));
     } else {
         const uint4 w0 = gv.recs[2 * k + 0], w1 = gv.recs[2 * k + 1];
         return make_float4(__uint_as_float(w0.w), __uint_as_float(w1.x), __uint_as_float(w1.y),
@@ -150,12 +151,15 @@ __device__ __forceinline__ void grid_rect(const GV& gv, const float4* __restrict
 #else
     constexpr bool kTwoWay = kXZ;
 #endif
-    const bool k0 = ak == 0u, k2 = kTwoWay ? !k0 : ak == 2u;
+    // compact (maze) records: x or z normal, y the first in-plane axis
+    // (grid_build.cpp), so k0 is one compare and (v, u) = (y, the other)
+    const bool k0 = kCompact ? meta < (1u << 20) : ak == 0u, k2 = kTwoWay ? !k0 : ak == 2u;
     const float ok = kTwoWay ? (k0 ? r.o.x : r.o.z) : sel_k(k0, k2, r.o);
     const float dk = kTwoWay ? (k0 ? r.d.x : r.d.z) : sel_k(k0, k2, r.d);
     const float yk = kTwoWay ? (k0 ? r.y.x : r.y.z) : sel_k(k0, k2, r.y);
-    const float ov = k0 ? r.o.y : r.o.x, dv = k0 ? r.d.y : r.d.x;
-    const float ou = k2 ? r.o.y : r.o.z, du = k2 ? r.d.y : r.d.z;
+    const float ov = kCompact ? r.o.y : (k0 ? r.o.y : r.o.x), dv = kCompact ? r.d.y : (k0 ? r.d.y : r.d.x);
+    const float ou = kCompact ? (k0 ? r.o.z : r.o.x) : (k2 ? r.o.y : r.o.z);
+    const float du = kCompact ? (k0 ? r.d.z : r.d.x) : (k2 ? r.d.y : r.d.z);
     const float4 th = rec_thresholds<kCompact>(gv, k, meta);
     const float a = qdiv(__uint_as_float(w.x) - ok, dk, yk);
     const float y1 = (ov - __uint_as_float(w.y)) + a * dv;
@@ -179,7 +183,8 @@ __device__ __forceinline__ float ax(F3 v) {
 template <int A, bool kCompact, typename GV>
 __device__ __forceinline__ void grid_rect_axis(const GV& gv, uint32_t k, uint4 w, const Ray& r, float& best,
                                                uint32_t& bk, uint32_t& tie) {
-    constexpr int V = A == 0 ? 1 : 0, U = A == 2 ? 1 : 2;
+    // (a compact z-normal record stores y first: grid_build.cpp)
+    constexpr int V = A == 0 ? 1 : (A == 2 && kCompact ? 1 : 0), U = A == 2 ? (kCompact ? 0 : 1) : 2;
     const float4 th = rec_thresholds<kCompact>(gv, k, w.w);
     const float a = qdiv(__uint_as_float(w.x) - ax<A>(r.o), ax<A>(r.d), ax<A>(r.y));
     const float y1 = (ax<V>(r.o) - __uint_as_float(w.y)) + a * ax<V>(r.d);
@@ -272,8 +277,22 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     int bx = grid_first(g, 0, r.o.x + s0 * r.d.x, r.y.x),
         by = kFlat ? (r.y.y > 0.0f ? 1 : 0) : grid_first(g, 1, r.o.y + s0 * r.d.y, r.y.y),
         bz = grid_first(g, 2, r.o.z + s0 * r.d.z, r.y.z);
+#ifndef MM_DIRECT_CELL_TIME
+    // Crossing time of boundary b along axis a in one fma per step:
+    // t = RN(b * B_a + A_a), A_a = RN(RN(mn_a - o_a) * y_a), B_a = RN(cell_a * y_a).
+    // Its error along axis a, |dt| * |d_a|, is a few u (|mn_a - o_a| + b cell_a
+    // + |x_a(t) - o_a|) <= ~8 u C (y_a = RN(1/d_a)); grid_time's direct form has
+    // ~5 u C.  Both are far below the lists' eps = 2^-14 C = 1024 u C, which is
+    // all the search's argument needs of them (header: delta + eta << eps).
+    const float Ax = (g.mn[0] - r.o.x) * r.y.x, Bx = g.cell[0] * r.y.x;
+    const float Az = (g.mn[2] - r.o.z) * r.y.z, Bz = g.cell[2] * r.y.z;
+    const float Ay = kFlat ? 0.0f : (g.mn[1] - r.o.y) * r.y.y, By = kFlat ? 0.0f : g.cell[1] * r.y.y;
+    float tx = __builtin_fmaf((float)bx, Bx, Ax), tz = __builtin_fmaf((float)bz, Bz, Az);
+    float ty = kFlat ? grid_time(g, 1, by, r.o.y, r.y.y) : __builtin_fmaf((float)by, By, Ay);
+#else
     float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
           tz = grid_time(g, 2, bz, r.o.z, r.y.z);
+#endif
     // Cell words (grid_build.cpp).  Wide (64-bit): bits 0-21 the list's first
     // entry; bit 63 set: bits 22-31 the count, the whole list for every face;
     // clear: bits 22-24 the count m <= 7, and per entry face f a 6-bit
@@ -281,6 +300,40 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // across f did not already hold.  Plain (32-bit): first | count << 22.
     // face = 6: the whole list (the first cell).  (A run-time format flag
     // cost 2 % on C3: the format is a template parameter.)
+#ifndef MM_NO_STEP_CELL
+    // The current cell's index, stepped with the walk (+-1 per x step, +-n0 per
+    // z step (n0 n1 in 3-D), +-n0 per y step), and the bit offset of each
+    // axis's entry-face field in the wide cell word (25 + 6 f; the face
+    // toward the previous cell is fixed per ray and axis), packed 8 bits per
+    // axis: x, y, z.
+    int ci;
+    {
+        const int ix = r.y.x > 0.0f ? bx - 1 : bx, iz = r.y.z > 0.0f ? bz - 1 : bz;
+        const int iy = kFlat ? 0 : (r.y.y > 0.0f ? by - 1 : by);
+        ci = kFlat ? iz * g.n[0] + ix : (iz * g.n[1] + iy) * g.n[0] + ix;
+    }
+    const int dcx = r.y.x > 0.0f ? 1 : -1;
+    const int dcz = (r.y.z > 0.0f ? 1 : -1) * (kFlat ? g.n[0] : g.n[0] * g.n[1]);
+    const int dcy = kFlat ? 0 : (r.y.y > 0.0f ? 1 : -1) * g.n[0];
+    const uint32_t fsh = (25u + (r.y.x > 0.0f ? 0u : 6u)) | ((37u + (r.y.y > 0.0f ? 0u : 6u)) << 8) |
+                         ((49u + (r.y.z > 0.0f ? 0u : 6u)) << 16);
+    // sh = 0: the whole list (the first cell)
+    auto cell_range = [&](uint32_t sh, uint32_t& j0, uint32_t& j1) {
+        const uint32_t c = (uint32_t)ci;
+        if constexpr (kWide) {
+            const uint64_t cw = reinterpret_cast<const uint64_t*>(gv.cells)[c];
+            const bool whole = (cw >> 63) != 0;
+            const uint32_t m = (uint32_t)(cw >> 22) & (whole ? 0x3FFu : 7u);
+            const uint32_t fld = sh ? (uint32_t)(cw >> sh) & 63u : (m << 3);
+            j0 = ((uint32_t)cw & 0x3FFFFFu) + (whole ? 0u : (fld & 7u));
+            j1 = j0 + (whole ? m : (fld >> 3));
+        } else {
+            const uint32_t cw = reinterpret_cast<const uint32_t*>(gv.cells)[c];
+            j0 = cw & 0x3FFFFFu;
+            j1 = j0 + (cw >> 22);
+        }
+    };
+#else
     auto cell_range = [&](uint32_t face, uint32_t& j0, uint32_t& j1) {
         const int ix = r.y.x > 0.0f ? bx - 1 : bx, iz = r.y.z > 0.0f ? bz - 1 : bz;
         const int iy = kFlat ? 0 : (r.y.y > 0.0f ? by - 1 : by);
@@ -298,8 +351,13 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             j1 = j0 + (cw >> 22);
         }
     };
+#endif
     uint32_t j, jend;
+#ifndef MM_NO_STEP_CELL
+    cell_range(0u, j, jend);
+#else
     cell_range(6u, j, jend);
+#endif
     uint32_t cells = 1, tests = g.n_glob;
     // One iteration: test one rect of the current cell; when the cell's list
     // is done, step to the next cell (or stop) in the same iteration.
@@ -330,14 +388,24 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             // (by-value selects: a select of two loads becomes a load of a
             // selected address -- of the kernel argument or a scratch copy)
             const int b = sx ? bx : (sy ? by : bz);
+            [[maybe_unused]] const float ya = sel_xy(sx, sy, r.y);
+#ifndef MM_DIRECT_CELL_TIME
+            const float nt = __builtin_fmaf((float)b, sel_xy(sx, sy, F3{Bx, By, Bz}), sel_xy(sx, sy, F3{Ax, Ay, Az}));
+#else
             const float mn = sel_xy(sx, sy, F3{g.mn[0], g.mn[1], g.mn[2]});
             const float cs = sel_xy(sx, sy, F3{g.cell[0], g.cell[1], g.cell[2]});
-            const float oa = sel_xy(sx, sy, r.o), ya = sel_xy(sx, sy, r.y);
+            const float oa = sel_xy(sx, sy, r.o);
             const float nt = ((mn + (float)b * cs) - oa) * ya;
+#endif
             tx = sx ? nt : tx;
             ty = sy ? nt : ty;
             tz = sz ? nt : tz;
+#ifndef MM_NO_STEP_CELL
+            ci += sx ? dcx : (sy ? dcy : dcz);
+            cell_range((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu, j, jend);
+#else
             cell_range((sx ? 0u : (sy ? 2u : 4u)) + (ya > 0.0f ? 0u : 1u), j, jend);  // (ya: by value, see above)
+#endif
             if (kStats) ++cells;
         }
     }

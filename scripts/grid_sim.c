@@ -159,7 +159,7 @@ static void build_grid(double cell_target) {
    every entry the neighbour across that face does not list */
 static uint32_t *fr_off, *fr_list;
 static uint8_t (*fr_s)[6], (*fr_l)[6];
-static int fr_on, start_on;
+static int fr_on, start_on, direct_on;
 static float start_t = 0.09375f;
 static int listed_in(long c, uint32_t k) {
     for (uint32_t q = cell_off[c]; q < cell_off[c + 1]; ++q) if (cell_list[q] == k) return 1;
@@ -168,7 +168,9 @@ static int listed_in(long c, uint32_t k) {
 static void build_faces(void) {
     fr_on = getenv("FACES") != NULL;
     start_on = getenv("START") != NULL;
-    if (start_on) start_t = (float)atof(getenv("START")) > 0.0f ? (float)atof(getenv("START")) : 0.09375f;
+    direct_on = getenv("DIRECT") != NULL;
+    /* START=1 (or 0): the kernel's t = 3/32; START=<t>: that t */
+    if (start_on) { start_t = (float)atof(getenv("START")); if (!(start_t > 0.0f) || start_t == 1.0f) start_t = 0.09375f; }
     long total = (long)gn[0] * gn[1] * gn[2];
     int ax0 = 0, ax1 = 2;  /* the plane: two axes with most cells */
     { int o[3] = {0, 1, 2};
@@ -252,6 +254,14 @@ static inline void consider(float a, uint32_t k, float* best, uint32_t* bk, int*
 #define MAXC 128
 static __thread int q_len[MAXC];   /* list lengths of the cells the last query visited */
 static __thread int q_n;
+/* crossing time of boundary b along axis a: the kernel's fma form (mm_grid.h,
+ * default) or, with DIRECT=1, the direct form ((mn + b cell) - o) * y */
+static float cell_time(int a, int b, float o, float y) {
+    if (direct_on) return (gmin[a] + (float)b * gcell[a] - o) * y;
+    const float A = (gmin[a] - o) * y, B = gcell[a] * y;
+    return fmaf((float)b, B, A);
+}
+
 static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
     float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, yy[3];
     for (int a = 0; a < 3; ++a) {
@@ -274,7 +284,7 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
         if (i > gn[a] - 1) i = gn[a] - 1;
         ic[a] = i;
         stp[a] = dd[a] > 0.0f ? 1 : -1;
-        tn[a] = (gmin[a] + (float)(i + (stp[a] > 0)) * gcell[a] - oo[a]) * yy[a];
+        tn[a] = cell_time(a, i + (stp[a] > 0), oo[a], yy[a]);
     }
     int ncell = 0;
     q_n = 0;
@@ -307,7 +317,7 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
         ic[a] += stp[a];
         face = 2 * a + (stp[a] > 0 ? 0 : 1);  /* entered through the face toward the previous cell */
         if (ic[a] < 0 || ic[a] >= gn[a]) break;
-        tn[a] = (gmin[a] + (float)(ic[a] + (stp[a] > 0)) * gcell[a] - oo[a]) * yy[a];
+        tn[a] = cell_time(a, ic[a] + (stp[a] > 0), oo[a], yy[a]);
     }
     st->cells += ncell;
     st->hist_cells[ncell < 63 ? ncell : 63]++;
