@@ -203,6 +203,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 #define MM_OPT_GRID_CELL  25  /* grid search: the first cell size tried, in percent of the median rect extent
                                   (25..400, default 100; coarser cells follow until the index fits the LDS
                                   budget).  Read by mm_upload_scene */
+#define MM_OPT_GRID_WIDE  26  /* grid search: 1 (default) 64-bit cell words with per-face list ranges where the
+                                  image fits the LDS budget; 0 plain 32-bit words (whole list per cell).  Read
+                                  by mm_upload_scene */
 #define MM_OPT_FAULT_INJECT 23 /* tests of the error path (results are then invalid): 0 off (default); 1 every
                                   wave-persistent launch raises an injected fault (error bit 3); 2 the tail
                                   rings' protocol waits give up at once (bit 2 when a wait was needed; the

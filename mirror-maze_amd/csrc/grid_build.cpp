@@ -339,7 +339,7 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
 // in LDS) fit index_budget bytes.
 bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
                 const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why, bool merge_axes,
-                double cell_scale) {
+                double cell_scale, bool wide) {
     if (n_rects == 0 || n_rects > 65535) { why = "rect count outside 1..65535"; return false; }
     std::vector<uint32_t> ident(n_rects), recs;
     for (uint32_t k = 0; k < n_rects; ++k) ident[k] = k;
@@ -412,7 +412,7 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         // 64-bit cell words with face ranges where the whole image fits the
         // budget, else plain 32-bit words at the same cell size, before
         // coarser cells (the kernel variant for wide words stages all of it)
-        if (build_lists(rects, n_rects, recs, smin, smax, C, s, true, merge_axes, g, why)) {
+        if (wide && build_lists(rects, n_rects, recs, smin, smax, C, s, true, merge_axes, g, why)) {
             if (maze_form(g)) compact_layout(g);
             if (g.bytes <= index_budget) break;
         }

@@ -35,8 +35,9 @@ struct GridHost {
 // Returns false (with a reason) when the scene does not suit the search.
 // merge_axes: an axis whose cells would not shorten the lists gets one cell (MM_OPT_GRID_MERGE).
 // cell_scale: the first cell size tried, in units of the median rect extent (MM_OPT_GRID_CELL).
+// wide: 64-bit cell words with per-face list ranges where they fit (MM_OPT_GRID_WIDE), else plain words.
 bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, uint32_t n_nodes,
                 const uint32_t* idx, size_t index_budget, GridHost& g, std::string& why, bool merge_axes = true,
-                double cell_scale = 1.0);
+                double cell_scale = 1.0, bool wide = true);
 
 }  // namespace mm

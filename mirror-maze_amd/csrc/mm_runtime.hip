@@ -119,6 +119,7 @@ struct mm_ctx {
     int opt_fault = 0;           // MM_OPT_FAULT_INJECT
     bool opt_grid_merge = true;  // MM_OPT_GRID_MERGE (read by mm_upload_scene)
     int opt_grid_cell = 100;     // MM_OPT_GRID_CELL (read by mm_upload_scene)
+    bool opt_grid_wide = true;   // MM_OPT_GRID_WIDE (read by mm_upload_scene)
     bool last_defer = false;     // the last trace call ran the tail rings
     int last_kern_mode = -1, last_kern_form = -1;  // for MM_INFO_LAST_VGPRS / _SCRATCH
     bool last_kern_defer = false;
@@ -487,6 +488,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_dict = (uint32_t)value;
             return MM_OK;
         case MM_OPT_GRID_MERGE: c->opt_grid_merge = value != 0; return MM_OK;
+        case MM_OPT_GRID_WIDE: c->opt_grid_wide = value != 0; return MM_OK;
         case MM_OPT_GRID_CELL:
             if (value < 25 || value > 400) return fail(c, MM_ERR_INVALID, "grid cell scale must be 25..400 (%)");
             c->opt_grid_cell = value;
@@ -649,7 +651,7 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     std::string gwhy;
     // (80 KB: the LDS of one of the two 1024-thread blocks per CU)
     const bool grid_ok = fast && build_grid(rects, n_rects, nodes, n_nodes, idx, 80 * 1024, gh, gwhy,
-                                            c->opt_grid_merge, c->opt_grid_cell / 100.0);
+                                            c->opt_grid_merge, c->opt_grid_cell / 100.0, c->opt_grid_wide);
     if (!fast) gwhy = "scene coordinates outside the exact-division guards";
     DevGrid dg{};
     if (grid_ok) {

@@ -36,6 +36,7 @@ MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS = 1, 2, 3, 7, 8
 MM_OPT_LDS_SPLIT, MM_OPT_FUSE_RESOLVE, MM_OPT_RESERVE_CUS, MM_OPT_DICT_NODES, MM_OPT_DEFER = 9, 12, 19, 20, 21
 MM_OPT_DEFER_MIN, MM_OPT_FAULT_INJECT, MM_OPT_GRID_MERGE, MM_OPT_GRID_CELL = 22, 23, 24, 25
+MM_OPT_GRID_WIDE = 26
 MM_PENDING = 1
 MM_TRAV_AUTO, MM_TRAV_IFIF, MM_TRAV_LEAF_INTERIOR, MM_TRAV_LEAN, MM_TRAV_GRID = -1, 0, 5, 7, 11
 MM_INFO_GRID_OK, MM_INFO_GRID_CELLS_X, MM_INFO_GRID_CELLS_Y, MM_INFO_GRID_CELLS_Z = 1, 2, 3, 4
