@@ -417,6 +417,31 @@ def test_grid_cell_formats(gpu):
         r.close()
 
 
+def test_plain_cell_words_option_bit_exact(gpu):
+    """MM_OPT_GRID_WIDE 0: C3's maze indexed with plain 32-bit cell words (the
+    whole list per cell) instead of per-face list ranges -- the format the
+    N=64 scene uses -- is 0 ulp against the oracle on C3 windows, with the
+    same ray count."""
+    from oracle.oracle import Oracle
+
+    from mirror_maze import MM_INFO_GRID_FACES, MM_INFO_GRID_OK, MM_OPT_GRID_WIDE, Renderer, default_uniform, make_ext
+
+    s = _scene(32)
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    r.set_option(MM_OPT_GRID_WIDE, 0)
+    r.upload_scene(s)
+    assert r.scene_info(MM_INFO_GRID_OK) == 1.0 and r.scene_info(MM_INFO_GRID_FACES) == 0.0
+    u = default_uniform(1920, 1080, 0)
+    e = make_ext(8, 8, 8, frame=2)
+    for (x0, y0) in [(0, 0), (944, 520), (1888, 1064), (300, 800)]:
+        got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
+        ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
+        assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
+        assert st.rays == rst.rays
+    r.close()
+
+
 def test_bench_prints_one_json_line(gpu):
     """bench.py's driver contract: exactly one JSON line on stdout with the
     metric, the roofline and the issue mode (short C2 run)."""
