@@ -319,7 +319,8 @@ def main():
     # one RCCL gather per frame, issued async on the frame's stream into
     # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
     # multi-frame launches need the wave-persistent kernel's fused resolve (64 % spp == 0)
-    # (with the mirror-tail deferral -- the default -- samples are staged per frame, any spp)
+    # (with the mirror-tail deferral -- MM_OPT_DEFER, or spp that does not divide 64 -- samples are staged per
+    # frame, any spp)
     batchable = not args.accumulate
     fb_max = (min(args.batch, max(args.steps, args.warmup, 8)) if args.batch > 0 else 8) if batchable else 1
     # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,

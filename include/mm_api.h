@@ -186,12 +186,11 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   their block's tail ring (512 entries) and the block's waves take 64 of them at
                                   a time as a chunk of their own; samples are then staged per path and resolved
                                   by k_resolve (same order).  0 off, 1..64; default: 32 when the search
-                                  structure sits whole in LDS (C3 3.26 ms vs 3.71 with 0) and bounce_limit >= 8
-                                  (C2's 4 bounces: 0.404 ms/frame on vs 0.384 off) or 64 % spp != 0 (samples
-                                  staged anyway), else off (the N=64
-                                  scene, records via L1/L2: C5 frame 227.7 ms off vs 231.4 on) --
-                                  profiles/r02_ab_ring.txt, r02_ab_defer_bounces.txt.  Built for the grid search and the lean BVH form
-                                  with records in LDS; other forms ignore it */
+                                  structure sits whole in LDS and 64 % spp != 0 (samples staged anyway), else
+                                  off (with the fused resolve the staging and the parked records cost more than
+                                  the dense tails save: C3 2.96 ms/frame off vs 3.04 on, C4 23.7 vs 24.5,
+                                  profiles/r03/ab_defer_off.txt).  Built for the grid search and the lean BVH
+                                  form with records in LDS; other forms ignore it */
 #define MM_OPT_DEFER_MIN  22  /* MM_OPT_DEFER applies to launches of at least this many paths (w*h*spp*frames;
                                   default 2^24: below it the staged resolve outweighs the tail saved -- C1
                                   0.039 vs 0.033 ms/frame, C2 x 5 frames 0.49 vs 0.42; 10 frames of rank 0 of an

@@ -920,15 +920,14 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         if (rc0) return rc0;
     }
     // mirror-tail deferral (MM_OPT_DEFER): samples staged per path, tails run from block-local rings; built for
-    // the grid search and the lean BVH form with records in LDS (other forms run without it)
-    // (auto: with the whole search structure in LDS -- the grid image, or BVH nodes + compact records; the N=64
-    // scene's records read through L1/L2 gain nothing from it: C5 frame 231.4 vs 227.7 ms without) and paths of
-    // at least 8 bounces (below, the staging + resolve outweigh the tail saved: C2's 4 bounces, 20 frames per
-    // launch, 0.404 vs 0.384 ms/frame; C3's 8: 3.25 vs 3.60 -- profiles/r02_ab_defer_bounces.txt) -- or samples
-    // that are staged anyway (64 % spp != 0: no fused resolve)
+    // the grid search and the lean BVH form with records in LDS (other forms run without it).  Auto: only where
+    // the samples are staged anyway (64 % spp != 0: no fused resolve) and the search structure sits whole in LDS.
+    // Round 2 had it on for paths of >= 8 bounces (C3 3.25 vs 3.60 ms/frame); with round 3's cheaper walk the
+    // staging, the resolve pass and the parked records' traffic cost more than the dense tails save (C3 20 frames
+    // per launch 2.957 vs 3.04 ms/frame, rank 0 of 8 0.387 vs 0.403, C4 23.66 vs 24.5, C5 frame 157.3 vs 162.3;
+    // profiles/r03/ab_defer_off.txt)
     const bool defer_on =
-        c->opt_defer > 0 ||
-        (c->opt_defer < 0 && (mode == 11 || mode == 3) && (e->bounce_limit >= 8u || 64 % e->spp != 0));
+        c->opt_defer > 0 || (c->opt_defer < 0 && (mode == 11 || mode == 3 || mode == 14) && 64 % e->spp != 0);
     const bool defer_built = persist && wavepersist_defer_built(mode, form);
     if (wave && !defer_built)
         return fail(c, MM_ERR_UNSUPPORTED, "MM_PIPE_WAVEFRONT: no tail-deferral kernel for this scene's query "

@@ -29,13 +29,13 @@ def _diff(got, ref):
     return int(bad.sum())
 
 
-@pytest.mark.parametrize("opts", [{22: 1 << 24}, {21: 0}], ids=["tail-deferral", "no-tail-deferral"])
+@pytest.mark.parametrize("opts", [{21: 32, 22: 1 << 24}, {21: 0}], ids=["tail-deferral", "no-tail-deferral"])
 def test_c3_bench_path_two_whole_frames(gpu, opts):
     """C3 as bench.py renders it: MM_PIPE_AUTO (the grid search), consecutive
     frames in ONE mm_trace_tile_frames launch, every pixel of both 1920x1080
     frames (2 x 137 M closest-hit queries) vs the oracle -- with mirror-tail
-    deferral through the block-local tail rings (the default past
-    MM_OPT_DEFER_MIN = 2^24 paths, as in bench.py's launches) and without it."""
+    deferral through the block-local tail rings (32 lanes, past
+    MM_OPT_DEFER_MIN = 2^24 paths) and without it (the default)."""
     from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 
@@ -101,7 +101,7 @@ def test_c4_rank0_of_eight_way_split(gpu):
 C5_WINDOWS = [(0, 0), (1904, 1064), (3808, 2144), (700, 1500), (2900, 300), (1200, 40)]
 
 
-@pytest.mark.parametrize("opts", [{}, {22: 0}, {7: 7}], ids=["auto", "auto-tail-deferral", "bvh-walk"])
+@pytest.mark.parametrize("opts", [{}, {21: 32, 22: 0}, {7: 7}], ids=["auto", "tail-deferral", "bvh-walk"])
 def test_c5_windows_64spp(gpu, opts):
     """C5: 64x64 maze, 3840x2160 frame coordinates, 64 spp, 16/16 bounces --
     the reference's 64-sample reduction (shaders.metal:342-364) as the fused
@@ -214,7 +214,7 @@ def test_cameras_inside_the_maze(gpu, cell, direction):
     e = make_ext(8, 8, 8, frame=3)
     ref, n = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 320, 180)
     assert n > 4 * 320 * 180 * 8 and ref[..., :3].mean() > 0.01  # the paths bounce inside the maze
-    for opts in ({}, {22: 0}):  # fused resolve; tail deferral with staged samples
+    for opts in ({}, {21: 32, 22: 0}):  # fused resolve; tail deferral with staged samples
         r = Renderer(0)
         r.set_pipeline(MM_PIPE_AUTO)
         for k, v in opts.items():

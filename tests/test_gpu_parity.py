@@ -116,7 +116,7 @@ PIPES = {
     "grid": (1, {7: 11}, False),
     "grid-nofuse": (1, {7: 11, 12: 0}, False),
     "grid-nodefer": (1, {21: 0}, False),
-    "grid-defer": (1, {22: 0}, False),                       # tail deferral (32 lanes) on any launch size
+    "grid-defer": (1, {21: 32, 22: 0}, False),               # tail deferral (32 lanes) on any launch size
     "grid-defer16": (1, {21: 16, 22: 0}, False),
     "grid-defer63": (1, {21: 63, 22: 0}, False),
     "grid-defer64": (1, {21: 64, 22: 0}, False),             # every path at bounce 1: tail rings run full
@@ -236,7 +236,7 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 0}, {22: 0}])
+@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 0}, {21: 32, 22: 0}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole
