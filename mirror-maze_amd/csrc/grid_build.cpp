@@ -423,6 +423,20 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     }
     g.n_slow = n_slow_g;
     g.flat_ok = maze_form(g);
+    g.slab = false;
+    if (g.n_glob == 2) {
+        const uint32_t m0 = grecs[8 * (size_t)g.glob[0] + 7], m1 = grecs[8 * (size_t)g.glob[1] + 7];
+        const bool y_fast = (m0 >> 30) == 0u && (m1 >> 30) == 0u && ((m0 >> 20) & 3u) == 1u && ((m1 >> 20) & 3u) == 1u;
+        float y0, y1;
+        std::memcpy(&y0, &grecs[8 * (size_t)g.glob[0]], 4);
+        std::memcpy(&y1, &grecs[8 * (size_t)g.glob[1]], 4);
+        if (y_fast && y0 != y1 && std::isfinite(y0) && std::isfinite(y1)) {
+            if (y1 < y0) { std::swap(g.glob[0], g.glob[1]); std::swap(y0, y1); }
+            g.slab = true;
+            g.slab_y[0] = y0;
+            g.slab_y[1] = y1;
+        }
+    }
     if (g.flat_ok) {
         g.n_class = (uint32_t)cls.size() / 4;
         compact_layout(g);

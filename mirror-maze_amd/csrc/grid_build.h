@@ -28,6 +28,11 @@ struct GridHost {
     // the thresholds in a class table at off_class) and the kernel walks x / z
     // with 2-way record selects.
     bool flat_ok = false;
+    // The two global rects are y-normal FAST records in the planes y = slab_y[0] < slab_y[1] (glob[0],
+    // glob[1]: the maze's floor and ceiling): a query tests only the one the ray is not moving away from
+    // (mm_grid.h grid_search).
+    bool slab = false;
+    float slab_y[2] = {0.0f, 0.0f};
     uint32_t off_class = 0, n_class = 0;
     std::vector<uint8_t> image;
 };

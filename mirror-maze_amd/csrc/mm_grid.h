@@ -259,10 +259,36 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
     uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
+#ifndef MM_NO_SLAB_GLOBALS
+    // Floor and ceiling (g.slab): a y-normal plane the ray moves away from
+    // gives a = RN(num / d_y) with num = RN(Y - o_y) on the wrong side of
+    // RN(0.05 d_y), so a <= 0.05 (1 + u) and a > 0.1 fails -- that rect
+    // cannot change (best, bk, tie).  When every lane can skip one of the
+    // two, each lane tests only the other (its record read per lane).
+    bool one = false;
+    uint32_t k1 = 0;
+    if (g.slab) {
+        const float q = 0.05f * r.d.y;
+        const bool lo_dead = r.d.y > 0.0f && g.slab_y[0] - r.o.y <= q;
+        const bool hi_dead = r.d.y < 0.0f && g.slab_y[1] - r.o.y >= q;
+        one = __builtin_amdgcn_ballot_w64(!(lo_dead || hi_dead)) == 0;
+        k1 = lo_dead ? g.glob[1] : g.glob[0];
+    }
+    if (one) {
+        MM_LANE_STAT(kLpGlobal);
+        grid_rect_axis<1, kFlat>(gv, k1, rec_words<kFlat>(gv, k1), r, best, bk, tie);
+    } else {
+        for (uint32_t j = 0; j < g.n_glob; ++j) {
+            MM_LANE_STAT(kLpGlobal);
+            grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
+        }
+    }
+#else
     for (uint32_t j = 0; j < g.n_glob; ++j) {
         MM_LANE_STAT(kLpGlobal);
         grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
     }
+#endif
     // The walk starts in the cell of the ray's point at t = 3/32, not at the
     // origin: a rect of A has a > 0.1, so the cells the ray occupies only for
     // t < 3/32 hold nothing it can return, and the rounding of the start
