@@ -55,7 +55,7 @@ struct GridQuery {
 // lanes together) grants them queue entries, those lanes stop and return true
 // with p holding the state the next bounce starts from.  defer_from >= 2^30:
 // never.
-template <bool kStats, bool kPool = false, typename Q, typename Reserve>
+template <bool kStats, typename Q, typename Reserve>
 __device__ __forceinline__ bool bounce_loop_r(const DevScene& sc, const Q& query, PathState& p, int bounce_limit,
                                               int mirror_limit, ScratchStack& stack, Counters& c, bool& overflow,
                                               int defer_from, uint32_t defer_lanes, Reserve&& reserve) {
@@ -74,7 +74,7 @@ __device__ __forceinline__ bool bounce_loop_r(const DevScene& sc, const Q& query
 #endif
         if (kStats) c.rays++;
         if (!ok) { overflow = true; break; }
-        const bool more = shade_step<kPool>(sc, p, t, k, mirror_limit);
+        const bool more = shade_step(sc, p, t, k, mirror_limit);
 #ifdef MM_PHASE_CLOCKS
         c.s_cyc += (uint64_t)wall_clock64() - t1;
 #endif
@@ -84,11 +84,11 @@ __device__ __forceinline__ bool bounce_loop_r(const DevScene& sc, const Q& query
 }
 
 // The bounce loop without deferral.
-template <bool kStats, bool kPool = false, typename Q>
+template <bool kStats, typename Q>
 __device__ __forceinline__ void bounce_loop(const DevScene& sc, const Q& query, PathState& p, int bounce_limit,
                                             int mirror_limit, ScratchStack& stack, Counters& c, bool& overflow) {
-    bounce_loop_r<kStats, kPool>(sc, query, p, bounce_limit, mirror_limit, stack, c, overflow, 1 << 30, 0u,
-                                 []() { return false; });
+    bounce_loop_r<kStats>(sc, query, p, bounce_limit, mirror_limit, stack, c, overflow, 1 << 30, 0u,
+                          []() { return false; });
 }
 
 // Whole path (shaders.metal:302-344): returns sqrt(max(L, 0)).

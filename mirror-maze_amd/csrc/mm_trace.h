@@ -478,97 +478,8 @@ struct PathState {
     int n, mh;
 };
 
-// Wave-pooled rejection sampling (the wave-persistent kernels, kPool).
-// shaders.metal:316-318 draws (x, y, z) = 3 random() until length <= 1; a wave
-// runs its unluckiest lane's ~6.5 trials where a lane needs 1.9 on average.
-// Pooled: after every lane's first trial, the lanes still rejecting ("owners",
-// n of them) publish their random() state in LDS, and each owner gets P = 2^lg
-// consecutive lanes (n P <= 64, P <= 32): lane L works for owner L >> lg on
-// trial (L & (P - 1)) + 1 past the owner's state -- the state jumped by 3 (L &
-// (P - 1)) draws, s -> A^k s + C_k (the LCG of random(), jump table in LDS).
-// An owner takes the first accepted trial of its lanes in trial order (its
-// (x, y, z), length^2 and post-trial state, by ds_bpermute) -- exactly the
-// trial the serial loop would stop at -- or, when all P were rejected (or a
-// lane of its run is inactive), advances its state past the trials done and
-// stays an owner.  Every value is computed by the same operations as the
-// serial loop's.  (MM_POOL_TRIALS; A/B: profiles/r03/ab_pool_trials.txt.)
-constexpr uint32_t kPoolJumps = 33;  // jumps of 3j draws, j = 0..32
-__device__ __forceinline__ uint32_t* pool_words() {
-    __shared__ uint32_t w[16 * 64 + 2 * kPoolJumps];  // per wave 64 owner states; then (A^3j, C_3j)
-    return w;
-}
-// The jump table; the block's first threads, before a __syncthreads.
-__device__ __forceinline__ void pool_init() {
-    if (threadIdx.x < kPoolJumps) {
-        uint32_t a = 1u, c = 0u;
-        for (uint32_t i = 0; i < 3u * threadIdx.x; ++i) {
-            a = a * 747796405u;
-            c = c * 747796405u + 291336453u;
-        }
-        pool_words()[16 * 64 + 2 * threadIdx.x] = a;
-        pool_words()[16 * 64 + 2 * threadIdx.x + 1] = c;
-    }
-}
-__device__ __forceinline__ uint32_t pool_jump(uint32_t s, uint32_t j) {
-    const uint32_t* t = pool_words() + 16 * 64 + 2 * j;
-    return t[0] * s + t[1];
-}
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ void pooled_trials(uint32_t& seed, F3& rd, float& len2) {
-    uint32_t* slot = pool_words() + 64u * (threadIdx.x >> 6);
-    const uint32_t lane = __lane_id();
-    for (;;) {
-        const bool need = len2 > 0x1.000002p0f;
-        const uint64_t R = __ballot(need);
-        if (R == 0) break;
-        const uint64_t A = __ballot(1);
-        const uint32_t n = (uint32_t)__popcll(R);
-        // P = 2^lg: n P <= 64, P <= 32
-        const uint32_t clog = n <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(n - 1u);
-        const uint32_t lg = min(6u - clog, 5u);
-        const uint32_t q_own = lane_rank(R);
-        if (need) slot[q_own] = seed;  // (one wave's LDS operations complete in order)
-        const uint32_t q = lane >> lg, j = lane & ((1u << lg) - 1u);
-        float wx = 0.0f, wy = 0.0f, wz = 0.0f, wl = 0.0f;
-        uint32_t ws = 0u;
-        const bool work = q < n;
-        if (work) {
-            ws = pool_jump(slot[q], j);
-            wx = rand_pm1(ws);
-            wy = rand_pm1(ws);
-            wz = rand_pm1(ws);
-            wl = dot3(F3{wx, wy, wz}, F3{wx, wy, wz});
-        }
-        const uint64_t acc = __ballot(work && !(wl > 0x1.000002p0f));
-        // owner q_own: lanes [q_own P, q_own P + P) ran its trials 1..P
-        const uint32_t base = q_own << lg, P = 1u << lg;
-        const uint64_t seg = (P == 64u) ? ~0ull : ((1ull << P) - 1ull);
-        const uint64_t sa = (acc >> base) & seg, sd = (A >> base) & seg;
-        const uint64_t stop = sa | (~sd & seg);  // first accepted trial or first lane that did not run
-        const uint32_t f = stop ? (uint32_t)__builtin_ctzll(stop) : P;
-        const bool got = need && f < P && ((sa >> f) & 1ull);
-        const int src = (int)((base + (f < P ? f : 0u)) << 2);
-        // (every active lane runs the permutes: their sources are active lanes)
-        const float gx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(wx)));
-        const float gy = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(wy)));
-        const float gz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(wz)));
-        const float gl = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(wl)));
-        const uint32_t gs = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)ws);
-        if (got) {
-            rd = F3{gx, gy, gz};
-            len2 = gl;
-            seed = gs;
-        } else if (need) {
-            seed = pool_jump(seed, f);  // f trials rejected
-        }
-    }
-}
-
 // One shading step after a closest-hit query (the body of shaders.metal:306-340
 // after line 307).  Returns false when the path terminates.
-template <bool kPool = false>
 __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, float t, uint32_t k, int mirror_limit) {
     if (!(t < kBig)) return false;                           // miss, shaders.metal:336-338
     MM_LANE_STAT(kLpShade);
@@ -594,16 +505,13 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         // for every binary32 x (exhaustive check: scripts/verify_sqrt_gt1.c)
         // (a wave-pooled form of this loop -- the unluckiest lanes' trials spread
         // over the others with jumps of the random() state -- was bit-exact and
-        // 12 % slower on C3, profiles/r02_ab_grid_salu.txt)
-        if constexpr (kPool) {
-            pooled_trials(p.seed, rd, len2);
-        } else {
-            while (len2 > 0x1.000002p0f) {
-                MM_LANE_STAT(kLpTrial);
-                rx = rand_pm1(p.seed); ry = rand_pm1(p.seed); rz = rand_pm1(p.seed);
-                rd = F3{rx, ry, rz};
-                len2 = dot3(rd, rd);
-            }
+        // slower: 12 % on C3 in round 2, 3.5 % in round 3 with LDS state
+        // broadcast + ds_bpermute results, profiles/r03/ab_pool_trials.txt)
+        while (len2 > 0x1.000002p0f) {
+            MM_LANE_STAT(kLpTrial);
+            rx = rand_pm1(p.seed); ry = rand_pm1(p.seed); rz = rand_pm1(p.seed);
+            rd = F3{rx, ry, rz};
+            len2 = dot3(rd, rd);
         }
         const F3 rn = rsq(len2) * rd;                        // %358
         x = rn + side * nn;                                  // %367

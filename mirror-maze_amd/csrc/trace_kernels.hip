@@ -280,13 +280,6 @@ __device__ __forceinline__ void poison(float4* samples, uint32_t slot, uint32_t 
     if (slot < n_slots) samples[slot] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.0f);
 }
 
-// Wave-pooled rejection sampling in the wave-persistent kernels (mm_trace.h pooled_trials).
-#ifdef MM_POOL_TRIALS
-constexpr bool kPoolTrials = true;
-#else
-constexpr bool kPoolTrials = false;
-#endif
-
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
                                                      float4* __restrict__ samples, unsigned long long* stats,
@@ -324,8 +317,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             p.n = 0;
             p.mh = 0;
             bool overflow = false;
-            bounce_loop<kStats, kPoolTrials>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c,
-                                             overflow);
+            bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow);
             if (overflow) atomicOr(err, kErrStack);
             s = path_value(p);
             if (!job.fuse) samples[fr * n_paths + path] = make_float4(s.x, s.y, s.z, 0.0f);
@@ -453,7 +445,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             MM_LANE_STAT(kLpChunk);
             bool overflow = false;
             uint32_t seq = 0;
-            const bool deferred = bounce_loop_r<kStats, kPoolTrials>(
+            const bool deferred = bounce_loop_r<kStats>(
                 sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
                 defer_from, job.defer_lanes, [&]() { return ring_reserve(seq); });
             if (overflow) atomicOr(err, kErrStack);
@@ -661,10 +653,6 @@ __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersis
         __syncthreads();
     }
     if (job.fault == 1u && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, kErrInjected);
-    if constexpr (kPoolTrials) {  // the jump table of the pooled trials
-        pool_init();
-        __syncthreads();
-    }
 #ifdef MM_LANE_STATS
     if (threadIdx.x < 2u * kLpCount) lane_stat_words()[threadIdx.x] = 0u;
     __syncthreads();
