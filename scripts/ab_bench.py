@@ -45,6 +45,8 @@ VARIANTS = {
     "ref": (3, {}),
     "cell60": (1, {25: 60}), "cell70": (1, {25: 70}), "cell80": (1, {25: 80}), "cell90": (1, {25: 90}),
     "cell110": (1, {25: 110}), "cell125": (1, {25: 125}), "cell140": (1, {25: 140}), "cell160": (1, {25: 160}),
+    "reserve64": (1, {19: 64}),     # MM_OPT_RESERVE_CUS: resident blocks on 192 of 256 CUs' worth
+    "reserve128": (1, {19: 128}),   # 128 of 256
     "plain": (1, {26: 0}),          # MM_OPT_GRID_WIDE 0: plain 32-bit cell words (whole list per cell)
     "nomerge": (1, {24: 0}),        # MM_OPT_GRID_MERGE 0: cells along y by the rect size (round 2's grid)
     "grid-global-nomerge": (1, {1: 0, 24: 0}),
