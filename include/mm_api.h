@@ -186,15 +186,16 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   their block's tail ring (512 entries) and the block's waves take 64 of them at
                                   a time as a chunk of their own; samples are then staged per path and resolved
                                   by k_resolve (same order).  0 off, 1..64; default: 32 when the search
-                                  structure sits whole in LDS and 64 % spp != 0 (samples staged anyway), else
-                                  off (with the fused resolve the staging and the parked records cost more than
-                                  the dense tails save: C3 2.96 ms/frame off vs 3.04 on, C4 23.7 vs 24.5,
-                                  profiles/r03/ab_defer_off.txt).  Built for the grid search and the lean BVH
+                                  structure sits whole in LDS (the maze grid with its leaf boxes, or BVH nodes +
+                                  compact records) and bounce_limit >= 8 (C3, 20 frames per launch: 2.64 ms/frame
+                                  on vs 2.74 off; C4 20.97 vs 21.80), or 64 % spp != 0 (samples staged anyway),
+                                  else off (the N=64 scene, leaf boxes via L1/L2: 5.23 on vs 4.90 off) --
+                                  profiles/r03/ab_defer_claims.txt.  Built for the grid search and the lean BVH
                                   form with records in LDS; other forms ignore it */
 #define MM_OPT_DEFER_MIN  22  /* MM_OPT_DEFER applies to launches of at least this many paths (w*h*spp*frames;
-                                  default 2^24: below it the staged resolve outweighs the tail saved -- C1
-                                  0.039 vs 0.033 ms/frame, C2 x 5 frames 0.49 vs 0.42; 10 frames of rank 0 of an
-                                  8-way C3 split, 20.7 M paths, 0.50 vs 0.51); 0: always */
+                                  default 2^26: below it the staged resolve and the rings' drain outweigh the
+                                  tails saved -- rank 0 of an 8-way C3 split, 20 frames = 41 M paths per
+                                  launch: 0.392 ms/frame on vs 0.377 off); 0: always */
 #define MM_OPT_GRID_MERGE 24  /* grid search: 1 (default) an axis whose cells would not shorten the lists
                                   gets one cell (the maze: one cell along y -- its walls span the height, the
                                   lower cell is the space below the floor); 0 cells per axis by the typical

@@ -35,7 +35,7 @@ def test_c3_bench_path_two_whole_frames(gpu, opts):
     frames in ONE mm_trace_tile_frames launch, every pixel of both 1920x1080
     frames (2 x 137 M closest-hit queries) vs the oracle -- with mirror-tail
     deferral through the block-local tail rings (32 lanes, past
-    MM_OPT_DEFER_MIN = 2^24 paths) and without it (the default)."""
+    MM_OPT_DEFER_MIN = 2^24 paths) and without it."""
     from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 
