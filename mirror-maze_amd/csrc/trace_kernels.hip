@@ -285,6 +285,37 @@ __device__ __forceinline__ void poison(float4* samples, uint32_t slot, uint32_t 
 #endif
 constexpr uint32_t kClaimChunks = MM_CLAIM_CHUNKS;  // chunks per dequeue (A/B: -DMM_CLAIM_CHUNKS=k)
 
+// The next 64-path chunk of the global queue for this wave (its first path;
+// >= n_queue: the queue is out).  Claims of kClaimChunks chunks per returning
+// device-scope atomicAdd while every wave of the grid could still take one more
+// such claim, then one chunk at a time: one counter word saturates at ~88
+// dequeues per us (MI355X_MICROARCH.md, "dequeue"), C3's chunk rate at one
+// chunk per claim (259,200 chunks in 2.95 ms; profiles/r03/ab_claim_chunks.txt).
+// The wave's claimed range [next, end) lives in LDS, not in registers held
+// across the bounce loop (SGPR pressure there spills into VGPR lanes).
+__device__ __forceinline__ uint32_t* claim_words() {
+    __shared__ uint32_t w[2 * 16];  // (next, end) per wave of a <= 1024-thread block
+    return w + 2 * (threadIdx.x >> 6);
+}
+__device__ __forceinline__ void claim_reset() {
+    if ((threadIdx.x & 63u) == 0) { claim_words()[0] = 0u; claim_words()[1] = 0u; }
+}
+__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
+    uint32_t* cw = claim_words();
+    uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
+    if (next >= end) {
+        const uint32_t big = kClaimChunks * 64u;
+        const uint32_t tail = gridDim.x * (blockDim.x >> 6) * big;  // paths left below which claims are single
+        const uint32_t k = (n_queue > tail && next < n_queue - tail) ? big : 64u;
+        uint32_t b = 0;
+        if ((threadIdx.x & 63u) == 0) b = atomicAdd(work, k);
+        next = __builtin_amdgcn_readfirstlane(b);
+        end = min(next + k, n_queue);
+    }
+    if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
+    return next;
+}
+
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
                                                      float4* __restrict__ samples, unsigned long long* stats,
@@ -298,25 +329,10 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     Counters c;
     ScratchStack stack;
     uint32_t paths = 0, chunks = 0;
-    // Dequeue in claims of kClaimChunks chunks while every wave of the grid
-    // could still take one more such claim, then one chunk at a time: one
-    // returning device-scope atomicAdd on one word saturates at ~88 dequeues
-    // per us (MI355X_MICROARCH.md, "dequeue"), which is C3's chunk rate at one
-    // chunk per claim (259,200 chunks in 2.95 ms).
-    const uint32_t big = kClaimChunks * 64u;
-    const uint32_t tail = gridDim.x * (blockDim.x >> 6) * big;  // paths left below which claims are single
-    uint32_t next = 0, end = 0;
+    claim_reset();
     for (;;) {
-        if (next >= end) {
-            const uint32_t k = (n_queue > tail && next < n_queue - tail) ? big : 64u;
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(work, k);
-            next = __builtin_amdgcn_readfirstlane(b);
-            end = min(next + k, n_queue);
-            if (next >= n_queue) break;
-        }
-        const uint32_t base = next;
-        next += 64u;
+        const uint32_t base = dequeue(work, n_queue);
+        if (base >= n_queue) break;
         ++chunks;
         const uint32_t qc = base >> 6;
         const uint32_t fr = job.n_frames > 1 ? qc / cpf : 0u;
@@ -391,10 +407,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
     ScratchStack stack;
     uint32_t paths = 0, chunks = 0;
     int defer_from = (int)job.defer_from;  // 2^30 (off) once the global queue is out
-    // new chunks from the global queue in claims of kClaimChunks, as in wavepersist_body
-    const uint32_t big = kClaimChunks * 64u;
-    const uint32_t tail = gridDim.x * (blockDim.x >> 6) * big;
-    uint32_t next = 0, end = 0;
+    claim_reset();
 #ifdef MM_RING_CLOCKS  // diagnostics: per wave (main chunks, tail chunks, claim retries) wall clock
     uint64_t rc_main = 0, rc_tail = 0, rc_idle = 0;
     uint64_t rc_t0 = 0;
@@ -420,18 +433,11 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
 #endif
                 continue;
             }
-            if (next >= end) {
-                const uint32_t kq = (n_queue > tail && next < n_queue - tail) ? big : 64u;
-                if (lane == 0) b = atomicAdd(work, kq);
-                next = __builtin_amdgcn_readfirstlane(b);
-                end = min(next + kq, n_queue);
-                if (next >= n_queue) {
-                    defer_from = 1 << 30;
-                    continue;
-                }
+            b = dequeue(work, n_queue);
+            if (b >= n_queue) {
+                defer_from = 1 << 30;
+                continue;
             }
-            b = next;
-            next += 64u;
         }
         ++chunks;
         PathState p;
