@@ -193,9 +193,9 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   profiles/r03/ab_defer_claims.txt.  Built for the grid search and the lean BVH
                                   form with records in LDS; other forms ignore it */
 #define MM_OPT_DEFER_MIN  22  /* MM_OPT_DEFER applies to launches of at least this many paths (w*h*spp*frames;
-                                  default 2^26: below it the staged resolve and the rings' drain outweigh the
-                                  tails saved -- rank 0 of an 8-way C3 split, 20 frames = 41 M paths per
-                                  launch: 0.392 ms/frame on vs 0.377 off); 0: always */
+                                  default 2^24: a single C3 frame (16.6 M paths) runs without the rings; rank
+                                  0 of an 8-way C3 split, 20 frames = 41 M paths per launch, 0.356 ms/frame
+                                  with them vs 0.362 without -- profiles/r03/emulated_scaling/); 0: always */
 #define MM_OPT_GRID_MERGE 24  /* grid search: 1 (default) an axis whose cells would not shorten the lists
                                   gets one cell (the maze: one cell along y -- its walls span the height, the
                                   lower cell is the space below the floor); 0 cells per axis by the typical

@@ -94,7 +94,7 @@ struct mm_ctx {
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
     uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
     int opt_defer = -1;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off, -1 auto)
-    uint32_t opt_defer_min = 1u << 26;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
+    uint32_t opt_defer_min = 1u << 24;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
     unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
     uint32_t wave_ts_cap = 0;
@@ -926,8 +926,8 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     // the grid search and the lean BVH form with records in LDS (other forms run without it).  Auto: with the
     // whole search structure in LDS (the maze grid with its leaf boxes, or BVH nodes + compact records) and paths
     // of >= 8 bounces, on launches of >= MM_OPT_DEFER_MIN paths (C3 20 frames per launch 2.64 vs 2.74 ms/frame,
-    // C4 20.97 vs 21.80; rank 0 of an 8-way C3 split, 41 M paths per launch: 0.392 vs 0.377 without -- under the
-    // 2^26 default; the N=64 scene, leaf boxes via L1/L2: 5.23 vs 4.90 without; profiles/r03/ab_defer_claims.txt),
+    // C4 20.97 vs 21.80, profiles/r03/ab_defer_claims.txt; rank 0 of an 8-way C3 split, 41 M paths per launch,
+    // 0.356 vs 0.362, profiles/r03/emulated_scaling/; the N=64 scene, leaf boxes via L1/L2: 5.23 vs 4.90 without),
     // or where the samples are staged anyway (64 % spp != 0)
     const bool defer_on =
         c->opt_defer > 0 ||
