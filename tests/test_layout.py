@@ -80,3 +80,20 @@ def test_integration_rust_binding_covers_the_declared_surface():
     bound = set(re.findall(r"pub fn (mm_[a-z_0-9]+)\s*\(", txt))
     declared = _declared_functions() - {"mm_layout_ok"}
     assert bound == declared, (declared - bound, bound - declared)
+
+
+def test_python_constants_match_the_header():
+    """Every MM_* constant the Python binding defines has the value
+    include/mm_api.h gives it (options, info keys, pipelines, error codes)."""
+    from mirror_maze import _lib
+
+    txt = (REPO / "include" / "mm_api.h").read_text()
+    header = {m.group(1): int(m.group(2), 0)
+              for m in re.finditer(r"^#define\s+(MM_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9A-Fa-f]+|\d+))\)?", txt, flags=re.M)}
+    mirrored = {k: getattr(_lib, k) for k in dir(_lib) if k.startswith("MM_") and isinstance(getattr(_lib, k), int)}
+    common = sorted(set(header) & set(mirrored))
+    assert len(common) >= 30, common
+    wrong = {k: (header[k], mirrored[k]) for k in common if header[k] != mirrored[k]}
+    assert not wrong, wrong
+    # the upload-time grid options the A/B tooling sets by number
+    assert header["MM_OPT_GRID_MERGE"] == 24 and header["MM_OPT_GRID_CELL"] == 25 and header["MM_OPT_GRID_WIDE"] == 26
