@@ -66,9 +66,11 @@ struct TileJob {
     // sync.  Null: the error flag stays sticky (parity mode reads it itself).
     uint32_t* status = nullptr;
     // Polls a tail-ring protocol wait may take before it gives up (error bit
-    // 2); the drain's wait for block-mates is bounded by lack of progress
-    // instead (trace_kernels.hip).  MM_OPT_FAULT_INJECT 2 sets 0.
-    uint32_t ring_spin = 1u << 21;
+    // 2; ~0.7 s -- 2^21, ~0.1 s, tripped once in a round-3 GPU run of the
+    // 64-lane deferral test, every path re-parked at every bounce); the drain
+    // does not wait for block-mates (trace_kernels.hip).  MM_OPT_FAULT_INJECT
+    // 2 sets 0.
+    uint32_t ring_spin = 1u << 24;
     // MM_OPT_FAULT_INJECT 1: the launch raises error bit 3 (tests of the
     // error path).
     uint32_t fault = 0;

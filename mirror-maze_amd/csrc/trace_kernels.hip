@@ -261,7 +261,7 @@ __device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
 
 // A protocol wait -- a reader for the writer of its entry, a writer for the
 // previous lap's reader -- waits on a step already under way, so it is
-// bounded (job.ring_spin polls, ~0.1 s): a protocol bug ends the launch with
+// bounded (job.ring_spin polls, ~0.7 s): a protocol bug ends the launch with
 // error bit 2 rather than a grid that never drains.  Returns false on timeout;
 // the caller then skips its load / store and poisons the sample slot it
 // knows (NaN), so the failure shows in the output as well as in the flag.
