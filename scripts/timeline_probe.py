@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--opt", action="append", default=[], help="MM_OPT key:value (repeatable)")
+    ap.add_argument("--batch", type=int, default=1, help="frames per launch (mm_trace_tile_frames), as bench.py")
     a = ap.parse_args()
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
     r = Renderer(0)
@@ -41,12 +42,19 @@ def main():
     print(f"# {desc}; times in us (wall_clock64, 100 MHz)")
     for n in [int(x) for x in a.ranks.split(",")]:
         y0, stride, rows = row_shard(H, n, 0)
-        out = torch.zeros((rows, W, 4), dtype=torch.float32, device="cuda")
-        r.trace_tile(u, make_ext(spp, bl, ml, frame=99), 0, y0, W, rows, y_stride=stride, out=out)
+        out = torch.zeros((a.batch, rows, W, 4), dtype=torch.float32, device="cuda")
+
+        def launch(frame):
+            if a.batch > 1:
+                r.trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), a.batch, 0, y0, W, rows, y_stride=stride,
+                                    out=out)
+            else:
+                r.trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, rows, y_stride=stride, out=out[0])
+        launch(99)
         for f in range(a.frames):
             ts.zero_()
             r.set_wave_timeline(ts)
-            r.trace_tile(u, make_ext(spp, bl, ml, frame=f), 0, y0, W, rows, y_stride=stride, out=out)
+            launch(f)
             torch.cuda.synchronize()
             r.set_wave_timeline(None)
             t = ts.cpu().numpy()
