@@ -939,9 +939,13 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                            "method / LDS placement (grid search, or BVH form 7 with nodes + "
                                            "records in LDS)");
     bool defer = defer_built && (defer_on || wave) && (wave || tile_paths * n_frames >= c->opt_defer_min);
-    // the tail ring's static LDS must leave two 1024-thread blocks per CU: a grid image within
-    // 2064 B of the 80 KB budget runs without the rings
-    if (defer && wavepersist_lds_bytes(sc, mode) + (4 + kTailRing) * sizeof(uint32_t) > 80 * 1024) {
+    // the deferral kernel's static LDS (tail ring, claimed queue ranges) must leave two 1024-thread blocks per
+    // CU: a grid image within that of the 80 KB budget runs without the rings
+    hipFuncAttributes dattr{};
+    const size_t defer_static = (defer && wavepersist_attributes(mode, form, true, &dattr) == hipSuccess)
+                                    ? dattr.sharedSizeBytes
+                                    : (4 + kTailRing) * sizeof(uint32_t) + 128;
+    if (defer && wavepersist_lds_bytes(sc, mode) + defer_static > 80 * 1024) {
         if (wave) return fail(c, MM_ERR_UNSUPPORTED, "MM_PIPE_WAVEFRONT: grid image + tail ring exceed the LDS budget");
         defer = false;
     }
