@@ -230,3 +230,35 @@ def test_staging_bound_for_multi_frame_launches(gpu):
         r.trace_tile_frames(u, make_ext(3, 8, 8), 87, 0, 0, 1920, 1080)
     r.sync()
     r.close()
+
+
+def test_auto_tail_deferral_policy(gpu):
+    """MM_OPT_DEFER auto (mm_runtime.hip): the tail rings run for paths of >= 8
+    bounces on launches of >= 2^24 paths where the maze grid sits whole in LDS
+    -- C3's 20-frame launches and rank 0's rows of an 8-way split (41 M paths)
+    -- and not on a single C3 frame (16.6 M paths), for 4-bounce paths (C2) or
+    on the N=64 scene (leaf boxes via L1/L2); MM_OPT_DEFER 0 turns it off."""
+    from mirror_maze import MM_INFO_LAST_DEFER, MM_INFO_LAST_LDS_MODE, Renderer, default_uniform, make_ext
+    from mirror_maze.dist import row_shard
+
+    u = default_uniform(1920, 1080, 0)
+    r = Renderer(0)
+    r.upload_scene(_scene(32))
+    r.trace_tile(u, make_ext(8, 8, 8, frame=0), 0, 0, 1920, 1080)  # one frame: 16.6 M paths
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 0.0 and r.scene_info(MM_INFO_LAST_LDS_MODE) == 11.0
+    y0, stride, rows = row_shard(1080, 8, 0)
+    r.trace_tile_frames(u, make_ext(8, 8, 8, frame=0), 20, 0, y0, 1920, rows, y_stride=stride)  # 41 M paths
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 1.0
+    r.trace_tile_frames(u, make_ext(8, 4, 4, frame=0), 2, 0, 0, 1920, 1080)  # 4-bounce paths
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 0.0
+    r.set_option(21, 0)
+    r.trace_tile_frames(u, make_ext(8, 8, 8, frame=0), 2, 0, 0, 1920, 1080)
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 0.0
+    r.sync()
+    r.close()
+    r = Renderer(0)
+    r.upload_scene(_scene(64))
+    r.trace_tile_frames(u, make_ext(8, 16, 16, frame=0), 2, 0, 0, 1920, 1080)
+    assert r.scene_info(MM_INFO_LAST_DEFER) == 0.0 and r.scene_info(MM_INFO_LAST_LDS_MODE) == 14.0
+    r.sync()
+    r.close()
