@@ -208,8 +208,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   by mm_upload_scene */
 #define MM_OPT_FAULT_INJECT 23 /* tests of the error path (results are then invalid): 0 off (default); 1 every
                                   wave-persistent launch raises an injected fault (error bit 3); 2 the tail
-                                  rings' protocol waits give up at once (bit 2 when a wait was needed; the
-                                  samples whose ring entries were skipped are NaN) */
+                                  rings' protocol waits give up at once (bit 2 when a wait was needed; a
+                                  writer that gives up leaves NaN in its sample, mm_last_error names the
+                                  first timed-out wait); 3 the trace call fails with MM_ERR_HIP after
+                                  taking its first launch's status slot, before the launch is enqueued */
 /* Default builds hold the kernels MM_PIPE_AUTO can select; values that need
  * the A/B-only variants (MM_OPT_PERSIST 0, MM_OPT_TRAVERSAL 0,
  * MM_OPT_LDS_SPLIT > 1, MM_OPT_DICT_NODES 2, BVH form 7 without nodes +

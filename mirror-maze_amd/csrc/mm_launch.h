@@ -66,11 +66,15 @@ struct TileJob {
     // sync.  Null: the error flag stays sticky (parity mode reads it itself).
     uint32_t* status = nullptr;
     // Polls a tail-ring protocol wait may take before it gives up (error bit
-    // 2; ~0.7 s -- 2^21, ~0.1 s, tripped once in a round-3 GPU run of the
-    // 64-lane deferral test, every path re-parked at every bounce); the drain
-    // does not wait for block-mates (trace_kernels.hip).  MM_OPT_FAULT_INJECT
-    // 2 sets 0.
-    uint32_t ring_spin = 1u << 24;
+    // 2; ~50 ms; a wait lasts at most a few bounces).  The round-3 trip of the
+    // 64-lane deferral test was a livelock ending at the 32-bit entry
+    // counters' wrap, not a slow wait (trace_kernels.hip).
+    // MM_OPT_FAULT_INJECT 2 sets 0.
+    uint32_t ring_spin = 1u << 20;
+    // The launch's first timed-out ring wait writes 16 words here
+    // (host-mapped; trace_kernels.hip ring_timeout); launch_id goes into it.
+    uint32_t* ring_diag = nullptr;
+    uint32_t launch_id = 0;
     // MM_OPT_FAULT_INJECT 1: the launch raises error bit 3 (tests of the
     // error path).
     uint32_t fault = 0;

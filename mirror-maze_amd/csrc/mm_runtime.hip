@@ -116,6 +116,7 @@ struct mm_ctx {
     struct Failed { uint64_t id; uint32_t bits; std::string what; bool reported; };
     std::deque<Call> pending;
     std::deque<Failed> failed;  // the last kFailedKept failed calls
+    uint64_t failed_dropped = 0;  // highest call id dropped from `failed` (older ids: status no longer kept)
     int opt_fault = 0;           // MM_OPT_FAULT_INJECT
     bool opt_grid_merge = true;  // MM_OPT_GRID_MERGE (read by mm_upload_scene)
     int opt_grid_cell = 100;     // MM_OPT_GRID_CELL (read by mm_upload_scene)
@@ -126,6 +127,7 @@ struct mm_ctx {
 };
 
 constexpr uint32_t kStatusSlots = 1024;
+constexpr uint32_t kRingDiagWords = 16;  // after the status words: the first timed-out ring wait's record
 constexpr size_t kFailedKept = 64;
 // Staged samples (tail deferral / no fused resolve) per launch: whole rows up
 // to this many paths (16 B each: 8 GiB).  A multi-frame launch over the cap
@@ -307,11 +309,29 @@ int next_status(mm_ctx* c, uint32_t*& dev_word) {
     return MM_OK;
 }
 
-std::string error_text(uint32_t bits) {
+// The record the launch's first timed-out ring wait left (trace_kernels.hip
+// ring_timeout), as text; consumed (a later trip writes a new one).
+std::string ring_diag_text(mm_ctx* c) {
+    uint32_t* d = c->h_status + kStatusSlots;
+    if (!__atomic_load_n(d, __ATOMIC_ACQUIRE)) return "";
+    uint32_t w[kRingDiagWords];
+    for (uint32_t i = 0; i < kRingDiagWords; ++i) w[i] = __atomic_load_n(d + i, __ATOMIC_RELAXED);
+    const uint64_t t0 = w[10] | (uint64_t)w[11] << 32, t1 = w[12] | (uint64_t)w[13] << 32;
+    char b[320];
+    snprintf(b, sizeof(b),
+             " [first timed-out wait (launch %u): %s of entry %u (slot %u, lap %u) in block %u wave %u lane %u "
+             "wanted turn %u, saw %u; reserved %u, claimed %u; %u polls over %.3f ms]",
+             w[15], w[1] == 1 ? "reader" : "writer", w[2], w[2] % kTailRing, w[2] / kTailRing, w[7], w[8], w[9],
+             w[3], w[4], w[5], w[6], w[14], (double)(t1 - t0) * 1e-5);
+    __atomic_store_n(d, 0u, __ATOMIC_RELEASE);
+    return b;
+}
+
+std::string error_text(mm_ctx* c, uint32_t bits) {
     std::string s;
-    auto add = [&](const char* m) { s += s.empty() ? m : std::string("; ") + m; };
+    auto add = [&](const std::string& m) { s += s.empty() ? m : std::string("; ") + m; };
     if (bits & kErrStack) add("traversal stack overflow (depth > 50)");
-    if (bits & kErrRing) add("tail ring wait timed out (kernel protocol error)");
+    if (bits & kErrRing) add("tail ring wait timed out (kernel protocol error)" + ring_diag_text(c));
     if (bits & kErrInjected) add("injected fault (MM_OPT_FAULT_INJECT)");
     return s.empty() ? "unknown error" : s;
 }
@@ -331,11 +351,21 @@ void poll_calls(mm_ctx* c) {
         }
         if (!done) { ++it; continue; }
         if (bits) {
-            c->failed.push_back({it->id, bits, it->what, false});
-            if (c->failed.size() > kFailedKept) c->failed.pop_front();
+            c->failed.push_back({it->id, bits, it->what + " -- " + error_text(c, bits), false});
+            if (c->failed.size() > kFailedKept) {
+                c->failed_dropped = std::max(c->failed_dropped, c->failed.front().id);
+                c->failed.pop_front();
+            }
         }
         it = c->pending.erase(it);
     }
+}
+
+// "call #N (what) failed on the GPU: why" (Failed::what holds "what -- why").
+std::string failed_text(const mm_ctx::Failed& f) {
+    const size_t k = f.what.find(" -- ");
+    return "call #" + std::to_string(f.id) + " (" + f.what.substr(0, k) + ") failed on the GPU: " +
+           (k == std::string::npos ? std::string("unknown error") : f.what.substr(k + 4));
 }
 
 // The oldest unreported failed call, as this call's return code.
@@ -344,9 +374,7 @@ int report_failure(mm_ctx* c, const char* suffix) {
     for (auto& f : c->failed)
         if (!f.reported) {
             f.reported = true;
-            return fail(c, error_code(f.bits),
-                        "call #" + std::to_string(f.id) + " (" + f.what + ") failed on the GPU: " +
-                            error_text(f.bits) + suffix);
+            return fail(c, error_code(f.bits), failed_text(f) + suffix);
         }
     return MM_OK;
 }
@@ -379,12 +407,12 @@ int mm_create(int device, mm_ctx** out) {
     if (rc == MM_OK) chk(hipMalloc((void**)&c->d_aux, 8 * sizeof(unsigned long long)), "hipMalloc(aux)");
     if (rc == MM_OK) chk(hipMemset(c->d_aux, 0, 8 * sizeof(unsigned long long)), "hipMemset(aux)");
     if (rc == MM_OK)
-        chk(hipHostMalloc((void**)&c->h_status, kStatusSlots * sizeof(uint32_t),
+        chk(hipHostMalloc((void**)&c->h_status, (kStatusSlots + kRingDiagWords) * sizeof(uint32_t),
                           hipHostMallocMapped | hipHostMallocCoherent),
             "hipHostMalloc(status)");
     if (rc == MM_OK) chk(hipHostGetDevicePointer((void**)&c->d_status, c->h_status, 0), "hipHostGetDevicePointer");
     if (rc == MM_OK) {
-        std::memset(c->h_status, 0, kStatusSlots * sizeof(uint32_t));
+        std::memset(c->h_status, 0, (kStatusSlots + kRingDiagWords) * sizeof(uint32_t));
         c->slot_owner.assign(kStatusSlots, 0);
     }
     if (rc != MM_OK) {
@@ -494,7 +522,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_grid_cell = value;
             return MM_OK;
         case MM_OPT_FAULT_INJECT:
-            if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "fault inject must be 0, 1 or 2");
+            if (value < 0 || value > 3) return fail(c, MM_ERR_INVALID, "fault inject must be 0..3");
             c->opt_fault = value;
             return MM_OK;
         default: return fail(c, MM_ERR_INVALID, "unknown option");
@@ -1014,46 +1042,66 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             job.defer_lanes = c->opt_defer > 0 ? (uint32_t)c->opt_defer : 32u;
             job.tail = tq;
         }
-        if ((rc = next_status(c, job.status))) return rc;
-        if ((rc = prof_mark(c))) return rc;
-        const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
-        if (persist) {
-            c->last_form = form >= kFormGrid ? kFormGrid : form;
-            c->last_mode = mode;
-            c->last_kern_mode = mode;
-            c->last_kern_form = form;
-            c->last_kern_defer = defer;
-            HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux, err_dev,
-                                             reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
-                                             c->stream));
-        } else {
-            MegaOpts mo;
-            mo.reference = c->pipe == MM_PIPE_REFERENCE;
-            mo.lds_nodes = lds_fits;
-            mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
-            HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux, err_dev, want_stats, mo, c->stream));
+        // The launch's status slot is taken first (its device address is a kernel argument); if the
+        // launch then fails to enqueue, the slot is released as finished-clean (a slot left
+        // owned by a launch that never runs would fail every later call on the context), and the call
+        // is still tracked below for the launches it did enqueue.
+        if ((rc = next_status(c, job.status))) break;
+        job.ring_diag = c->d_status + kStatusSlots;
+        job.launch_id = (uint32_t)(c->launch_seq - 1);
+        bool enqueued = false;
+        rc = [&]() -> int {
+            if (int r = prof_mark(c)) return r;
+            if (c->opt_fault == 3) return fail(c, MM_ERR_HIP, "injected enqueue failure (MM_OPT_FAULT_INJECT 3)");
+            const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
+            if (persist) {
+                c->last_form = form >= kFormGrid ? kFormGrid : form;
+                c->last_mode = mode;
+                c->last_kern_mode = mode;
+                c->last_kern_form = form;
+                c->last_kern_defer = defer;
+                HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux, err_dev,
+                                                 reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
+                                                 c->stream));
+            } else {
+                MegaOpts mo;
+                mo.reference = c->pipe == MM_PIPE_REFERENCE;
+                mo.lds_nodes = lds_fits;
+                mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
+                HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux, err_dev, want_stats, mo,
+                                          c->stream));
+                HIPC(c, launch_publish_status(err_dev, job.status, c->stream));
+            }
+            enqueued = true;
+            return prof_mark(c);
+        }();
+        if (!enqueued) {
+            c->h_status[(c->launch_seq - 1) % kStatusSlots] = kStatusDone;  // nothing will write this slot
+            break;
         }
-        if ((rc = prof_mark(c))) return rc;
-        if (!persist) HIPC(c, launch_publish_status(err_dev, job.status, c->stream));
-        if (fuse) {
-            launches += 1;
-            continue;
-        }
+        launches += fuse ? 1 : 2;
+        if (rc) break;
+        if (fuse) continue;
         // the frames' staged samples and output slices are contiguous (a multi-frame launch is one
         // row batch), so one resolve over h x n_frames rows covers them all
         TileJob rj = job;
         if (defer) rj.h = job.h * n_frames;
-        HIPC(c, launch_resolve(rj, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream));
-        launches += 2;
+        const hipError_t re =
+            launch_resolve(rj, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream);
+        if (re != hipSuccess) {
+            rc = fail(c, MM_ERR_HIP, std::string("launch_resolve: ") + hipGetErrorString(re));
+            break;
+        }
     }
     c->last_defer = defer;
-    {
+    if (c->launch_seq > first_launch) {  // the launches this call enqueued (all of them unless rc)
         char what[160];
         snprintf(what, sizeof(what), "%s, frames %u..%u, tile (%u, %u) %ux%u / %u, %u spp", n_frames > 1 ?
                  "mm_trace_tile_frames" : "mm_trace_tile", e->frame, e->frame + n_frames - 1, x0, y0, w, h,
                  y_stride, e->spp);
         c->pending.push_back({call_id, first_launch, c->launch_seq - first_launch, what, 0u});
     }
+    if (rc) return rc;
     if ((rc = end_timing(c, launches))) return rc;
     if (want_stats) {
         if ((rc = read_aux(c, stats))) return rc;
@@ -1097,10 +1145,14 @@ int mm_call_status(mm_ctx* c, uint64_t call_id) {
     for (auto& f : c->failed)
         if (f.id == call_id) {
             f.reported = true;
-            return fail(c, error_code(f.bits), "call #" + std::to_string(f.id) + " (" + f.what +
-                                                   ") failed on the GPU: " + error_text(f.bits));
+            return fail(c, error_code(f.bits), failed_text(f));
         }
-    return MM_OK;  // finished clean (or failed so long ago that it is no longer kept)
+    // a finished call not in the failed list: clean -- unless failed calls as old as it were dropped from the list
+    if (call_id <= c->failed_dropped)
+        return fail(c, MM_ERR_INVALID, "mm_call_status: status of call #" + std::to_string(call_id) +
+                                           " no longer kept (older than the last " + std::to_string(kFailedKept) +
+                                           " failed calls)");
+    return MM_OK;
 }
 
 int mm_set_profiling(mm_ctx* c, int enable) {

@@ -198,18 +198,40 @@ __device__ __forceinline__ F3 path_value(const PathState& p) {
 // unused, then one turn word per slot.  Entry n lives in slot
 // n % kTailRing; its writer waits for turn == 2 * lap (the previous lap's
 // reader is done), writes the payload, sets 2 * lap + 1; its reader waits for
-// that, loads, sets 2 * lap + 2.  A writer reserves only entries whose
-// previous-lap entry is claimed and a reader claims only reserved entries, so
-// every wait is on an operation of a smaller entry number that is already
-// under way -- no cycle.  Only waves of one block (one CU) touch a ring:
-// workgroup-scope release / acquire order the payload, no L2 writeback or
-// invalidate.
+// that, loads, sets 2 * lap + 2 (turn values modulo 2^24, ring_turn_value).  A
+// writer reserves only entries whose previous-lap entry is claimed and a
+// reader claims only reserved entries, so every wait is on an operation of a
+// smaller entry number that is already under way -- no cycle (and no cycle
+// through the SIMT rule either: a reader's 64 entries and a writer's <= 64
+// are within 127 of each other, a lap is 512).  Progress: every claim of
+// tails runs at least one bounce (wavepersist_ring_body).  Only waves of one
+// block (one CU) touch a ring: workgroup-scope release / acquire order the
+// payload, no L2 writeback or invalidate.  Protocol model:
+// tests/ring_model/ring_model.cpp (tests/test_ring_model.py).
+//
+// Memory ordering of the payload: the release of a turn
+// word is a plain ds_write_b32 with no s_waitcnt vmcnt before it -- the
+// writer's four global_store_dwordx4 and the reader's four
+// global_load_dwordx4 are still in flight when it issues (DESIGN.md s4 quotes
+// the ISA).  That is LLVM's AMDGPU memory model for a workgroup-scope release
+// on gfx94x/gfx950 outside threadgroup-split mode (.amdhsa_tg_split 0 here):
+// all waves of a work-group use the same vector L1, which serves a CU's
+// vector memory requests in order, so a later load by a block-mate that has
+// seen the turn word cannot pass the earlier stores; no wait is needed.
 __device__ __forceinline__ uint32_t* ring_ctl() {
     __shared__ uint32_t words[4 + kTailRing];
     return words;
 }
 __device__ __forceinline__ uint32_t* ring_turn(uint32_t seq) { return ring_ctl() + 4 + (seq % kTailRing); }
 __device__ __forceinline__ uint32_t ring_lap(uint32_t seq) { return seq / kTailRing; }
+// 2 * lap + c modulo 2^24: the entry counters are 32-bit, so lap wraps from
+// 2^32 / kTailRing - 1 = 2^23 - 1 to 0 and 2 * lap + 2 = 2^24 must read as the
+// next lap's 0 (without the mask the first writer after the wrap waits for 0
+// while its slot holds 2^24: the round-3 timeout, tests/test_ring_model.py).
+static_assert(kTailRing == 512, "turn values are taken modulo 2 * 2^32 / kTailRing");
+__device__ __forceinline__ uint32_t ring_turn_value(uint32_t seq, uint32_t c) {
+    return (2u * ring_lap(seq) + c) & 0xFFFFFFu;
+}
 
 __device__ __forceinline__ uint32_t lds_ld(uint32_t* a) {
     return __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -261,19 +283,45 @@ __device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
 
 // A protocol wait -- a reader for the writer of its entry, a writer for the
 // previous lap's reader -- waits on a step already under way, so it is
-// bounded (job.ring_spin polls, ~0.7 s): a protocol bug ends the launch with
-// error bit 2 rather than a grid that never drains.  Returns false on timeout;
-// the caller then skips its load / store and poisons the sample slot it
-// knows (NaN), so the failure shows in the output as well as in the flag.
-__device__ __forceinline__ bool ring_wait(uint32_t* turn, uint32_t want, uint32_t* err, uint32_t spin) {
-    for (uint32_t i = 0; lds_ld(turn) != want; ++i) {
-        if (i >= spin) {
-            atomicOr(err, kErrRing);
+// bounded (job.ring_spin polls, ~50 ms): a protocol bug ends the launch with
+// error bit 2 rather than a grid that never drains, and the launch's first
+// timed-out wait leaves a record of itself (ring_timeout).  Returns false on
+// timeout; the caller then skips its load / store.
+//
+// The record (TileJob::ring_diag, host-mapped, 16 words; mm_last_error prints
+// it): [0] 1 = written, [1] role (1 reader, 2 writer), [2] entry seq, [3]
+// wanted turn value, [4] the turn value last seen, [5] reserved, [6] claimed,
+// [7] block, [8] wave, [9] lane, [10..11] wall clock at the wait's first
+// failed poll, [12..13] at the timeout (100 MHz), [14] polls, [15] launch id.
+__device__ __noinline__ void ring_timeout(const TileJob& job, uint32_t* err, uint32_t role, uint32_t seq,
+                                          uint32_t want, uint32_t seen, uint64_t t0, uint32_t polls) {
+    if (atomicOr(err, kErrRing) & kErrRing) return;  // not the launch's first timeout
+    uint32_t* d = job.ring_diag;
+    if (!d) return;
+    const uint64_t t1 = wall_clock64();
+    d[1] = role; d[2] = seq; d[3] = want; d[4] = seen;
+    d[5] = lds_ld(ring_ctl() + 0); d[6] = lds_ld(ring_ctl() + 1);
+    d[7] = blockIdx.x; d[8] = threadIdx.x >> 6; d[9] = threadIdx.x & 63u;
+    d[10] = (uint32_t)t0; d[11] = (uint32_t)(t0 >> 32); d[12] = (uint32_t)t1; d[13] = (uint32_t)(t1 >> 32);
+    d[14] = polls; d[15] = job.launch_id;
+    __threadfence_system();
+    __hip_atomic_store(d, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ bool ring_wait(uint32_t seq, uint32_t c, uint32_t role, const TileJob& job, uint32_t* err) {
+    uint32_t* turn = ring_turn(seq);
+    const uint32_t want = ring_turn_value(seq, c);
+    uint64_t t0 = 0;
+    for (uint32_t i = 0;; ++i) {
+        const uint32_t seen = lds_ld(turn);
+        if (seen == want) return true;
+        if (i == 0) t0 = wall_clock64();
+        if (i >= job.ring_spin) {
+            ring_timeout(job, err, role, seq, want, seen, t0, i);
             return false;
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    return true;
 }
 
 __device__ __forceinline__ void poison(float4* samples, uint32_t slot, uint32_t n_slots) {
@@ -447,15 +495,13 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             live = lane < k;
             if (live) {
                 const uint32_t seq = __builtin_amdgcn_readfirstlane(first) + lane;
-                const uint32_t lap = ring_lap(seq);
                 const uint32_t rec = blockIdx.x * kTailRing + seq % kTailRing;
-                if (ring_wait(ring_turn(seq), 2u * lap + 1u, err, job.ring_spin)) {
+                if (ring_wait(seq, 1u, 1u, job, err)) {
                     slot = tail_load(tq, rec, p);
-                    // (the release waits for the loads above)
-                    __hip_atomic_store(ring_turn(seq), 2u * lap + 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {  // the record was never written: poison the slot it names (if in range) and skip it
-                    poison(samples, tq.rec[4u * (size_t)rec + 3u].z, n_slots);
-                    live = false;
+                    __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 2u), __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {  // the record was never written (its sample slot is unknown here: ADVICE r03): skip it;
+                    live = false;  // the error bit fails the call
                 }
             }
         } else {  // new paths
@@ -481,15 +527,20 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             MM_LANE_STAT(kLpChunk);
             bool overflow = false;
             uint32_t seq = 0;
+            // A claimed tail chunk of <= defer_lanes paths runs with deferral off: it would re-park at the top of
+            // its first bounce without running it, and a wave alone in its block could cycle the same tails
+            // through the ring forever (round 3, 64-lane deferral: tests/test_ring_model.py).  In the main phase
+            // a claim takes 64 tails, so this is off at defer_lanes < 64; every claim runs >= 1 bounce.
+            const int df = (k && k <= job.defer_lanes) ? (1 << 30) : defer_from;
             const bool deferred = bounce_loop_r<kStats>(
                 sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow,
-                defer_from, job.defer_lanes, [&]() { return ring_reserve(seq); });
+                df, job.defer_lanes, [&]() { return ring_reserve(seq); });
             if (overflow) atomicOr(err, kErrStack);
             if (deferred) {
-                const uint32_t lap = ring_lap(seq);
-                if (ring_wait(ring_turn(seq), 2u * lap, err, job.ring_spin)) {
+                if (ring_wait(seq, 0u, 2u, job, err)) {
                     tail_store(tq, blockIdx.x * kTailRing + seq % kTailRing, p, slot);
-                    __hip_atomic_store(ring_turn(seq), 2u * lap + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 1u), __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {
                     poison(samples, slot, n_slots);
                 }

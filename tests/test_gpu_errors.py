@@ -10,7 +10,10 @@ caused them, and valid long paths raise none.
   -- by mm_sync, by the next trace call (which is then not enqueued) and by
   mm_call_status -- never blamed on a later call.
 * Ring protocol timeouts (MM_OPT_FAULT_INJECT 2: waits give up at once) are
-  reported, and the samples they skipped are NaN in the image."""
+  reported with a record of the first stuck wait.
+* The round-3 tail-ring livelock (a lone wave cycling 64 tails, 64-lane
+  deferral) is gone; a failed enqueue releases its status slot; the status of
+  a call older than the kept failures is not reported clean."""
 from __future__ import annotations
 
 import numpy as np
@@ -171,7 +174,14 @@ def test_pending_status_is_visible_without_waiting(gpu):
     r.close()
 
 
-def test_ring_timeouts_are_reported_and_poison_the_skipped_samples(gpu):
+def test_ring_timeouts_are_reported_with_the_stuck_entry(gpu):
+    """MM_OPT_FAULT_INJECT 2: every protocol wait gives up at its first failed
+    poll.  The call fails by name, mm_last_error carries the launch's first
+    timed-out wait (trace_kernels.hip ring_timeout: role, entry, wanted and
+    seen turn values, the ring's counters), and a writer that gave up leaves
+    NaN in its sample."""
+    import re
+
     from mirror_maze import MMError, Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
 
@@ -191,17 +201,114 @@ def test_ring_timeouts_are_reported_and_poison_the_skipped_samples(gpu):
         failed = False
     except MMError as ex:
         failed = True
-        assert f"call #{call} " in str(ex) and "tail ring wait timed out" in str(ex)
+        msg = str(ex)
+        assert f"call #{call} " in msg and "tail ring wait timed out" in msg
+        m = re.search(r"first timed-out wait \(launch \d+\): (reader|writer) of entry (\d+) \(slot (\d+), lap (\d+)\) "
+                      r"in block \d+ wave (\d+) lane (\d+) wanted turn (\d+), saw (\d+); reserved (\d+), claimed (\d+)",
+                      msg)
+        assert m, msg
+        role, seq, slot, lap, wave, lane, want, seen, res, cl = m.groups()
+        seq, want, seen, res, cl = map(int, (seq, want, seen, res, cl))
+        assert int(slot) == seq % 512 and int(lap) == seq // 512 and int(wave) < 16 and int(lane) < 64
+        assert want == (2 * (seq // 512) + (1 if role == "reader" else 0)) and seen != want
+        assert cl <= res and seq < res
     img = got.cpu().numpy()
-    if failed:
-        assert np.isnan(img[..., :3]).any()  # a skipped sample shows in its pixel
-    else:  # no wait was ever needed: the image is exact
+    if not failed:  # no wait was ever needed: the image is exact
         ref, _ = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 256, 144)
         assert np.array_equal(_bits(img), _bits(ref))
     # the context works normally afterwards
     again, _ = r.trace_tile(u, e, 0, 0, 256, 144)
     r.sync()
     assert np.isfinite(again.cpu().numpy()).all()
+    r.close()
+
+
+def test_lone_wave_with_64_lane_deferral_terminates(gpu):
+    """The round-3 livelock (tests/test_ring_model.py): one 64-path chunk in a
+    closed room (every path survives its first bounce), deferral at 64 lanes.
+    The wave parks its 64 paths at bounce 1; its 15 block-mates found the
+    queue empty and have left; in round 3 it then claimed the 64 tails and
+    re-parked them at the top of their first bounce, forever (the launch ended
+    ~2^26 cycles later at the 32-bit counter wrap with a ring timeout).  Now a
+    claimed chunk of <= defer_lanes tails runs with deferral off: the call
+    ends in milliseconds, clean and bit-exact."""
+    import time
+
+    from mirror_maze import MM_INFO_LAST_DEFER, Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = closed_room(40, 0.2, 3)
+    r = Renderer(0)
+    r.set_option(21, 64)
+    r.set_option(22, 0)
+    r.upload_scene(s)
+    u = default_uniform(64, 64, 0)
+    for i in range(3):
+        u.cam.center[i] = 0.0
+    e = make_ext(8, 8, 8, frame=0)
+    for rep in range(3):
+        t0 = time.time()
+        got, st = r.trace_tile(u, e, 20 + rep, 30, 8, 1, stats=True)  # 64 paths: one chunk, one block
+        r.sync()
+        dt = time.time() - t0
+        assert r.scene_info(MM_INFO_LAST_DEFER) == 1.0
+        assert dt < 2.0, dt
+        ref, rays = oracle_tile(Oracle.from_scene(s), u, e, 20 + rep, 30, 8, 1)
+        assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref))
+        assert st.rays == rays
+    r.close()
+
+
+def test_failed_enqueue_releases_its_status_slot(gpu):
+    """a call that took a status slot and then failed to enqueue
+    its launch (MM_OPT_FAULT_INJECT 3) must not leave the slot owned: the next
+    1100 calls (more than the 1024 slots) run clean."""
+    from mirror_maze import MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.upload_scene(_scene(10))
+    u = default_uniform(64, 64, 0)
+    e = make_ext(1, 1, 1)
+    r.trace_tile(u, e, 0, 0, 8, 8)
+    r.set_option(23, 3)
+    with pytest.raises(MMError) as ei:
+        r.trace_tile(u, e, 0, 0, 8, 8)
+    assert "injected enqueue failure" in str(ei.value)
+    r.set_option(23, 0)
+    for i in range(1100):
+        r.trace_tile(u, e, 0, 0, 8, 8)
+    r.sync()
+    assert r.call_status(r.last_call()) is True
+    r.close()
+
+
+def test_status_of_calls_older_than_the_failed_list_is_not_reported_clean(gpu):
+    """mm_call_status keeps the last 64 failed calls; for an older
+    call it no longer knows the outcome of, it says so instead of MM_OK."""
+    from mirror_maze import MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.upload_scene(_scene(10))
+    u = default_uniform(64, 64, 0)
+    e = make_ext(8, 8, 8)
+    r.trace_tile(u, e, 0, 0, 8, 8)
+    clean = r.last_call()
+    r.set_option(23, 1)
+    ids = []
+    for i in range(70):
+        r.trace_tile(u, e, 0, 0, 8, 8)
+        ids.append(r.last_call())
+    r.set_option(23, 0)
+    with pytest.raises(MMError):
+        r.sync()  # reports the oldest unreported failure
+    with pytest.raises(MMError) as ei:
+        r.call_status(ids[0])  # dropped from the list of 64
+    assert "no longer kept" in str(ei.value)
+    with pytest.raises(MMError) as ei:
+        r.call_status(ids[-1])  # still kept: its own failure
+    assert "injected fault" in str(ei.value)
+    with pytest.raises(MMError):
+        r.call_status(clean)  # older than a dropped failure: unknown, not clean
     r.close()
 
 
