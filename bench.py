@@ -130,16 +130,12 @@ def launch_sizes(count: int, per_launch: int) -> list:
     return sizes
 
 
-def cpu_baseline(scene, u, ext, W, H, budget_s):
-    """Oracle (CPU restatement, oracle/mm_oracle.c -O2 scalar) on a bounded row
-    sample of the same workload, one thread per core, GIL released in C."""
-    from oracle.oracle import Oracle
-
-    o = Oracle.from_scene(scene)
-    threads, basis = usable_cpus()
-    # calibrate on one row, then pick a row sample that fits the budget
+def _cpu_rate(o, u, ext, W, H, budget_s, threads):
+    """Rays/s of Oracle `o` over a bounded row sample of the frame: calibrated
+    on one row, then every stride-th row on `threads` threads (GIL released in
+    C).  Returns (rays, seconds, sample text, seconds per row)."""
     t0 = time.perf_counter()
-    _, st = o.trace_tile(u, ext, 0, H // 2, W, 1)
+    o.trace_tile(u, ext, 0, H // 2, W, 1)
     row_s = max(time.perf_counter() - t0, 1e-6)
     rows = int(max(threads, min(H, budget_s * threads / row_s)))
     stride = max(1, H // rows)
@@ -165,6 +161,24 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
         t.join()
     dt = time.perf_counter() - t0
     rays = sum(totals)
+    return rays, dt, f"{len(sample_rows)} of {H} rows (every {stride}th) x {W} px x {ext.spp} spp, " \
+                     f"{rays} rays in {dt:.1f} s", row_s
+
+
+def cpu_baseline(scene, u, ext, W, H, budget_s):
+    """Two CPU baselines on the host cores, each on a bounded row sample of the
+    same workload, one thread per core:
+    * the oracle (oracle/mm_oracle.c, scalar C -O2): the reference's algorithm,
+      the BVH walk on every query (kind "port"), plus its single-core rate;
+    * same_algorithm (oracle/grid_cpu.c): the oracle's path loop with the
+      product's certified grid search as the query -- the GPU's algorithm on the
+      CPU, so the GPU / CPU ratio can be read with the algorithm held fixed.
+    Both return the reference walk's answers (identical images)."""
+    from oracle.oracle import Oracle
+
+    o = Oracle.from_scene(scene)
+    threads, basis = usable_cpus()
+    rays, dt, sample, row_s = _cpu_rate(o, u, ext, W, H, budget_s, threads)
     # the same loop on one core (SURVEY 8d asks for both), ~budget/4 seconds of rows
     n1 = int(max(1, min(H, budget_s / 4 / row_s)))
     t0 = time.perf_counter()
@@ -173,12 +187,17 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
         _, s1 = o.trace_tile(u, ext, 0, y, W, 1)
         rays1 += s1.rays
     dt1 = time.perf_counter() - t0
+    og = Oracle.from_scene(scene, method="grid")
+    grays, gdt, gsample, _ = _cpu_rate(og, u, ext, W, H, budget_s / 2, threads)
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "cores_basis": basis,
             "kind": "port",
-            "sample": f"{len(sample_rows)} of {H} rows (every {stride}th) x {W} px x {ext.spp} spp, "
-                      f"{rays} rays in {dt:.1f} s; scalar C oracle -O2 -ffp-contract=off",
+            "sample": f"{sample}; scalar C oracle -O2 -ffp-contract=off (the reference BVH walk per query)",
             "single_core": {"value": round(rays1 / dt1 / 1e6, 3), "unit": "Mrays/s",
                             "sample": f"{n1} rows, {rays1} rays in {dt1:.1f} s"},
+            "same_algorithm": {"value": round(grays / gdt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+                               "kind": "same-algorithm",
+                               "sample": f"{gsample}; oracle/grid_cpu.c: the certified grid search (the GPU's "
+                                         f"query method) in the oracle's path loop, scalar C -O2"},
             "host_cpus": os.cpu_count()}
 
 
@@ -285,14 +304,14 @@ def main():
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[args.config]
     scene = Scene.build(maze_n, 0)
     # Issue modes.  Every launch ends in a ~0.4 ms tail in which the last waves
-    # finish their last chunks (profiles/r01_timeline_probe.txt) -- 4 % of a
+    # finish their last chunks (profiles/r01/timeline_probe.txt) -- 4 % of a
     # C3 frame, 25 % of a rank's frame at N = 8.  Default (--batch 32): frames
     # are independent, so up to 32 consecutive frames share ONE launch's work
     # queue (mm_trace_tile_frames) and the tail is paid once per launch.
     # --batch 1: one frame per launch, optionally alternating over two
     # renderer contexts on their own streams so frame k+1's blocks fill the
     # CUs frame k's tail leaves idle (two frames sharing the GPU run ~7 %
-    # slower, profiles/r01_overlap_probe.txt; --contexts 0 times both).
+    # slower, profiles/r01/overlap_probe.txt; --contexts 0 times both).
     n_ctx = (1 if args.accumulate else args.contexts if args.contexts > 0 else 1 if args.batch > 1 else 2)
     rens = []
     for _ in range(n_ctx):

@@ -144,7 +144,7 @@ int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
                                   fully flattened pipeline
                                   (SoA state in HBM, one extend/shade launch pair per bounce) measured
                                   ~45 ms vs 5.7 ms per C3 frame and was retired (DESIGN.md §4,
-                                  profiles/r02_wavefront_pmc.txt) */
+                                  profiles/r02/wavefront_pmc.txt) */
 #define MM_PIPE_REFERENCE  3   /* straight statement of the reference kernel
                                   (IEEE division everywhere); A/B baseline  */
 int  mm_set_pipeline(mm_ctx* ctx, int pipe);

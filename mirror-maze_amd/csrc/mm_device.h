@@ -92,7 +92,8 @@ struct DevGrid {
     const uint4* image;        // the whole image (16-B units)
     uint32_t off_list, off_recs, off_box, bytes;  // section offsets in bytes
     // Compact records (maze grids, grid_build.cpp): 16 B per rect -- o_k, o_v,
-    // o_u, axis | class << 24 | kind << 30 -- and the folded thresholds of
+    // o_u, meta = class << 4 (bits 4-9: the class's byte offset into the
+    // class table) | axis << 20 | kind << 30 -- and the folded thresholds of
     // each class (Yv_lo, Yv_hi, Yu_lo, Yu_hi) in a table after the records.
     const float4* cls;
     uint32_t off_class;        // 0: 32-B records (no class table)

@@ -109,8 +109,9 @@ __device__ __forceinline__ GridView<C, L, R, B, K> grid_view(C c, L l, R r, B b,
 
 // Rect k's record: w = (o_k, o_v, o_u, meta) -- meta's axis at bit 20, kind at
 // bit 30 -- and its folded thresholds (Yv_lo, Yv_hi, Yu_lo, Yu_hi).  32-B
-// records hold both; compact records (kCompact, maze grids) hold w and a
-// class index (meta bits 24-29) into the class table.
+// records hold both; compact records (kCompact, maze grids) hold w and their
+// class as class << 4 (meta bits 4-9, meta & 0x3F0 = the byte offset of the
+// class's 16-B entry in the class table; grid_build.cpp).
 template <bool kCompact, typename GV>
 __device__ __forceinline__ uint4 rec_words(const GV& gv, uint32_t k) {
     if constexpr (kCompact) {
@@ -297,7 +298,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // a cell face; from the origin the walk would start on the far side of
     // that face in about half the cases and test a cell the ray never enters
     // (t = 1/16: C3 3.40 -> 3.37 ms/frame, C5 scene 7.20 -> 7.05; 3/32: a
-    // further 1.3 % / 1.4 %; bit-identical; profiles/r02_ab_start_cell.txt).
+    // further 1.3 % / 1.4 %; bit-identical; profiles/r02/ab_start_cell.txt).
     // The crossing times stay those of the origin.
     const float s0 = 0.09375f;
     int bx = grid_first(g, 0, r.o.x + s0 * r.d.x, r.y.x),

@@ -140,7 +140,7 @@ __device__ __forceinline__ float aabb_test(float4 a, float4 b, const Ray& r, flo
 // axis: a = (mn.x, mx.x, mn.y, mx.y), b = (mn.z, mx.z, packed, 0).  Scalar
 // ops: gfx950's v_pk_fma_f32 runs at the same FLOP rate as v_fma_f32 and the
 // register pairs cost occupancy (measured 13.6 vs 12.85 ms/frame on C3,
-// profiles/r01_ab_packed.txt).  Same values as aabb_test.
+// profiles/r01/ab_packed.txt).  Same values as aabb_test.
 template <bool kFast>
 __device__ __forceinline__ float aabb_pairs(float4 a, float4 b, const Ray& r, float t) {
     const float tx1 = sdiv<kFast>(a.x - r.o.x, r.d.x, r.y.x), tx2 = sdiv<kFast>(a.y - r.o.x, r.d.x, r.y.x);
@@ -336,7 +336,7 @@ __device__ __forceinline__ bool traverse(const DevScene& sc, const V& v, const R
 // node, that node's step.  Per lane the sequence of leaf tests, node visits,
 // pushes and pops is exactly the if-if loop's; a leaf visit just no longer
 // costs the wave an iteration of its own (C3 11.06 -> 10.37 ms,
-// profiles/r01_ab_leafinterior.txt).
+// profiles/r01/ab_leafinterior.txt).
 template <bool kFast, bool kStats, typename V>
 __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, const Ray& r, float& t,
                                             uint32_t& index, ScratchStack& stack, Counters& c) {
@@ -379,7 +379,7 @@ __device__ __forceinline__ bool traverse_li(const DevScene& sc, const V& v, cons
 // kind branches) and pushes skip the overflow test (upload rejects trees
 // deeper than the stack; near-first traversal holds at most one pending far
 // child per level).  Per lane the operation sequence is traverse_li's
-// (C3 10.40 -> 9.53 ms, profiles/r01_ab_lean.txt).
+// (C3 10.40 -> 9.53 ms, profiles/r01/ab_lean.txt).
 template <bool kStats, typename V>
 __device__ __forceinline__ bool traverse_lil(const DevScene& sc, const V& v, const Ray& r, float& t,
                                              uint32_t& index, ScratchStack& stack, Counters& c) {

@@ -722,7 +722,7 @@ hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s)
 
 // 1024-thread blocks at 8 waves per SIMD (<= 64 VGPRs).  With the grid search,
 // 768-thread blocks at 6 waves (80 VGPRs, no VGPR spills) measured 6.21 vs
-// 5.87 ms on C3 (profiles/r02_ab_grid_variants.txt).  (A/B builds:
+// 5.87 ms on C3 (profiles/r02/ab_grid_variants.txt).  (A/B builds:
 // -DMM_WP_THREADS=896 -DMM_WP_WAVES=7 and the like.)
 #ifndef MM_WP_THREADS
 #define MM_WP_THREADS 1024

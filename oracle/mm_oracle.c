@@ -219,6 +219,15 @@ static void intersect_bvh(ray_t* b, const oracle_scene* sc, trav_t* tr) {
     }
 }
 
+/* The closest-hit query of the path loop: the reference walk, or -- in
+ * grid_cpu.c's build (the bench's same-algorithm CPU baseline, not a checker)
+ * -- the product's certified grid search with this walk as its fallback. */
+#ifdef ORACLE_QUERY_FN
+static void ORACLE_QUERY_FN(ray_t* b, const oracle_scene* sc, trav_t* tr);
+#else
+#define ORACLE_QUERY_FN intersect_bvh
+#endif
+
 /* Metal sign(): 1, -1, +-0 for +-0, 0 for NaN */
 static inline float msign(float x) {
     if (x > 0.0f) return 1.0f;
@@ -236,7 +245,7 @@ static v3 trace_path(const oracle_scene* sc, v3 ori, v3 dir, uint32_t seed,
     v3 T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
     int mh = 0;
     for (int n = 0; n < bounce_limit + mh; ++n) {
-        intersect_bvh(&b, sc, tr);
+        ORACLE_QUERY_FN(&b, sc, tr);
         (*rays)++;
         if (tr->overflow) break;
         if (!(b.t < BIG)) break;                               /* miss: shaders.metal:336-338 */

@@ -13,6 +13,9 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "libmm_oracle.so"
+# bench.py's same-algorithm CPU baseline (grid_cpu.c): the oracle's path loop with the product's certified
+# grid search as the closest-hit query -- not a checker
+GRID_LIB_PATH = HERE / "_build" / "libmm_gridcpu.so"
 
 
 class _U(C.Structure):  # mm_uniform, include/mm_types.h
@@ -31,42 +34,62 @@ class Stats(C.Structure):
 
 
 _lib = None
+_grid_lib = None
 
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
 
 
+def _bind(path):
+    if not path.exists():
+        build()
+    return _declare(C.CDLL(str(path)))
+
+
+def grid_lib():
+    """The same-algorithm CPU baseline's library (grid_cpu.c; bench.py only)."""
+    global _grid_lib
+    if _grid_lib is None:
+        L = _bind(GRID_LIB_PATH)
+        L.gridcpu_build.argtypes = [C.c_void_p]
+        L.gridcpu_build.restype = C.c_int
+        _grid_lib = L
+    return _grid_lib
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not LIB_PATH.exists():
-            build()
-        L = C.CDLL(str(LIB_PATH))
-        P = C.c_void_p
-        L.oracle_trace_chunks.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
-        L.oracle_trace_group.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
-        L.oracle_trace_tile.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
-        L.oracle_trace_path.argtypes = [P, P, P, C.c_uint32, C.c_int, C.c_int, P, P]
-        L.oracle_rand_pm1.argtypes = [P]
-        L.oracle_rand_pm1.restype = C.c_float
-        L.oracle_seed_reference.argtypes = [C.c_uint32] * 3
-        L.oracle_seed_reference.restype = C.c_uint32
-        L.oracle_tile_seed.argtypes = [C.c_uint32] * 3
-        L.oracle_tile_seed.restype = C.c_uint32
-        L.oracle_primary_dir.argtypes = [P, C.c_uint32, C.c_uint32, P]
-        L.oracle_intersect_aabb.argtypes = [P, P, C.c_float, P, P]
-        L.oracle_intersect_aabb.restype = C.c_float
-        L.oracle_present_blur.argtypes = [P, P, C.c_uint32, C.c_uint32]
-        L.oracle_present_blur.restype = None
-        L.oracle_quantize.argtypes = [P, P, C.c_uint64]
-        L.oracle_quantize.restype = None
-        L.oracle_set_fp_mode.argtypes = [C.c_int]
-        L.oracle_set_fp_mode.restype = None
-        L.oracle_fp_flags.argtypes = [C.c_int]
-        L.oracle_fp_flags.restype = C.c_uint
-        _lib = L
+        _lib = _bind(LIB_PATH)
     return _lib
+
+
+def _declare(L):
+    """Argument and result types of the oracle entry points."""
+    P = C.c_void_p
+    L.oracle_trace_chunks.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+    L.oracle_trace_group.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+    L.oracle_trace_tile.argtypes = [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, P]
+    L.oracle_trace_path.argtypes = [P, P, P, C.c_uint32, C.c_int, C.c_int, P, P]
+    L.oracle_rand_pm1.argtypes = [P]
+    L.oracle_rand_pm1.restype = C.c_float
+    L.oracle_seed_reference.argtypes = [C.c_uint32] * 3
+    L.oracle_seed_reference.restype = C.c_uint32
+    L.oracle_tile_seed.argtypes = [C.c_uint32] * 3
+    L.oracle_tile_seed.restype = C.c_uint32
+    L.oracle_primary_dir.argtypes = [P, C.c_uint32, C.c_uint32, P]
+    L.oracle_intersect_aabb.argtypes = [P, P, C.c_float, P, P]
+    L.oracle_intersect_aabb.restype = C.c_float
+    L.oracle_present_blur.argtypes = [P, P, C.c_uint32, C.c_uint32]
+    L.oracle_present_blur.restype = None
+    L.oracle_quantize.argtypes = [P, P, C.c_uint64]
+    L.oracle_quantize.restype = None
+    L.oracle_set_fp_mode.argtypes = [C.c_int]
+    L.oracle_set_fp_mode.restype = None
+    L.oracle_fp_flags.argtypes = [C.c_int]
+    L.oracle_fp_flags.restype = C.c_uint
+    return L
 
 
 class Oracle:
@@ -82,9 +105,21 @@ class Oracle:
                               self.nodes.shape[0], self.idx.ctypes.data, self.is_mirror.ctypes.data,
                               self.emission.ctypes.data)
 
+        self._lib = lib
+
     @classmethod
-    def from_scene(cls, s) -> "Oracle":
-        return cls(s.rects, s.nodes, s.idx, s.is_mirror, s.emission)
+    def from_scene(cls, s, method: str = "walk") -> "Oracle":
+        """method "walk": the oracle (the reference BVH walk on every query);
+        "grid": the same path loop with the product's certified grid search as
+        the query (grid_cpu.c) -- bench.py's same-algorithm CPU baseline."""
+        o = cls(s.rects, s.nodes, s.idx, s.is_mirror, s.emission)
+        if method == "grid":
+            if grid_lib().gridcpu_build(C.byref(o.sc)) != 0:
+                raise RuntimeError("gridcpu_build failed")
+            o._lib = grid_lib
+        elif method != "walk":
+            raise ValueError(method)
+        return o
 
     @staticmethod
     def _u(uniform) -> bytes:
@@ -97,7 +132,7 @@ class Oracle:
         ch = np.ascontiguousarray(chunks, dtype=np.uint32).reshape(-1, 2)
         ub = C.create_string_buffer(bytes(uniform), len(bytes(uniform)))
         st = Stats()
-        rc = lib().oracle_trace_chunks(C.byref(self.sc), ub, ch.ctypes.data, ch.shape[0], tg[0], tg[1],
+        rc = self._lib().oracle_trace_chunks(C.byref(self.sc), ub, ch.ctypes.data, ch.shape[0], tg[0], tg[1],
                                        fb.ctypes.data, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_trace_chunks rc={rc}")
@@ -107,7 +142,7 @@ class Oracle:
         ch = np.ascontiguousarray(chunks, dtype=np.uint32).reshape(-1, 2)
         ub = C.create_string_buffer(bytes(uniform), len(bytes(uniform)))
         st = Stats()
-        rc = lib().oracle_trace_group(C.byref(self.sc), ub, ch.ctypes.data, ch.shape[0], tg[0], tg[1], gx, gy,
+        rc = self._lib().oracle_trace_group(C.byref(self.sc), ub, ch.ctypes.data, ch.shape[0], tg[0], tg[1], gx, gy,
                                       fb.ctypes.data, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_trace_group rc={rc}")
@@ -119,7 +154,7 @@ class Oracle:
         ub = C.create_string_buffer(bytes(uniform), len(bytes(uniform)))
         eb = C.create_string_buffer(bytes(ext), len(bytes(ext)))
         st = Stats()
-        rc = lib().oracle_trace_tile(C.byref(self.sc), ub, eb, x0, y0, w, h, y_stride, out.ctypes.data, C.byref(st))
+        rc = self._lib().oracle_trace_tile(C.byref(self.sc), ub, eb, x0, y0, w, h, y_stride, out.ctypes.data, C.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle_trace_tile rc={rc}")
         return out, st
@@ -129,7 +164,7 @@ class Oracle:
         dd = np.asarray(d, dtype=np.float32)
         rgb = np.zeros(3, dtype=np.float32)
         rays = C.c_uint32()
-        rc = lib().oracle_trace_path(C.byref(self.sc), o.ctypes.data, dd.ctypes.data, seed, bounce_limit,
+        rc = self._lib().oracle_trace_path(C.byref(self.sc), o.ctypes.data, dd.ctypes.data, seed, bounce_limit,
                                      mirror_limit, rgb.ctypes.data, C.byref(rays))
         return rgb, rays.value, rc
 

@@ -5,7 +5,7 @@ traces --frames frames in one multi-frame launch (bench.py's issue mode) when
 the fused resolve applies, else one launch per frame.
 
     python scripts/ab_bench.py [--config c3] [--frames 5] [--reps 2] [variant ...]
-A different build of the library: MIRROR_MAZE_LIB=/path/lib.so (scripts/ab_libs.sh).
+A different build of the library: MIRROR_MAZE_LIB=/path/lib.so (scripts/ab.py).
 """
 from __future__ import annotations
 

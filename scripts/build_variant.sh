@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build the product library from a git revision (or the working tree: "wt")
 # into exp/<name>/lib.so, optionally with extra hipcc flags, for A/B runs
-# (scripts/ab_libs.sh).  Usage: bash scripts/build_variant.sh <name> <rev|wt> [EXTRA flags...]
+# (scripts/ab.py).  Usage: bash scripts/build_variant.sh <name> <rev|wt> [EXTRA flags...]
 set -e
 NAME=$1; REV=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

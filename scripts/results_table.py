@@ -3,7 +3,7 @@
 rates, the VALU roofline of the reference-walk model, the SURVEY 8(d) HBM
 model) from bench.py JSON lines.
 
-    python scripts/results_table.py gpurun_out/<tag>/*.json > profiles/r02_results_table.md
+    python scripts/results_table.py gpurun_out/<tag>/*.json > profiles/r02/results_table.md
 """
 import json
 import sys

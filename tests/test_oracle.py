@@ -144,3 +144,35 @@ def test_reduction_order_is_reference_tree():
                 s.append(rgb.astype(f32))
             acc = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))
             assert np.array_equal((acc / f32(8)).view(np.uint32), img8[j, i, :3].view(np.uint32))
+
+
+def test_same_algorithm_cpu_baseline_equals_the_oracle():
+    """oracle/grid_cpu.c (bench.py's same-algorithm CPU baseline: the oracle's
+    path loop with the product's certified grid search as the query) returns
+    the reference walk's answers: bit-identical rows and the same ray counts
+    on the C2 / C3 / C5-scene mazes and the parity-mode dispatch of the
+    reference scene."""
+    import sys
+
+    sys.path.insert(0, str(GOLDEN.parent.parent / "mirror-maze_amd"))
+    from mirror_maze import ChunkScheduler, Scene, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    for n, (spp, b, m) in [(16, (1, 4, 15)), (32, (8, 8, 8)), (64, (2, 16, 16))]:
+        s = Scene.build(n, 0)
+        u = default_uniform(1920, 1080, 0)
+        e = make_ext(spp, b, m, frame=3)
+        walk, sw = Oracle.from_scene(s).trace_tile(u, e, 0, 530, 1920, 1)
+        grid, sg = Oracle.from_scene(s, method="grid").trace_tile(u, e, 0, 530, 1920, 1)
+        assert np.array_equal(walk.view(np.uint32), grid.view(np.uint32)), n
+        assert sw.rays == sg.rays
+    s = Scene.build(10, 0)
+    u = default_uniform(1024, 768, 1)
+    chunks = ChunkScheduler(1024, 768, 4, seed=3).next(768)
+    ow, og = Oracle.from_scene(s), Oracle.from_scene(s, method="grid")
+    fw, fg = np.zeros((768, 1024, 4), np.float32), np.zeros((768, 1024, 4), np.float32)
+    for gx, gy in [(0, 0), (5, 3), (31, 23), (17, 11)]:  # threadgroups of the reference dispatch
+        ow.trace_group(u, chunks, gx, gy, fw)
+        og.trace_group(u, chunks, gx, gy, fg)
+    assert fw[..., 3].sum() == 4 * 16
+    assert np.array_equal(fw.view(np.uint32), fg.view(np.uint32))
