@@ -316,13 +316,13 @@ std::string ring_diag_text(mm_ctx* c) {
     if (!__atomic_load_n(d, __ATOMIC_ACQUIRE)) return "";
     uint32_t w[kRingDiagWords];
     for (uint32_t i = 0; i < kRingDiagWords; ++i) w[i] = __atomic_load_n(d + i, __ATOMIC_RELAXED);
-    const uint64_t t0 = w[10] | (uint64_t)w[11] << 32, t1 = w[12] | (uint64_t)w[13] << 32;
+    const uint64_t t1 = w[12] | (uint64_t)w[13] << 32;
     char b[320];
     snprintf(b, sizeof(b),
              " [first timed-out wait (launch %u): %s of entry %u (slot %u, lap %u) in block %u wave %u lane %u "
-             "wanted turn %u, saw %u; reserved %u, claimed %u; %u polls over %.3f ms]",
+             "wanted turn %u, saw %u; reserved %u, claimed %u; gave up after %u polls at device clock %llu]",
              w[15], w[1] == 1 ? "reader" : "writer", w[2], w[2] % kTailRing, w[2] / kTailRing, w[7], w[8], w[9],
-             w[3], w[4], w[5], w[6], w[14], (double)(t1 - t0) * 1e-5);
+             w[3], w[4], w[5], w[6], w[14], (unsigned long long)t1);
     __atomic_store_n(d, 0u, __ATOMIC_RELEASE);
     return b;
 }

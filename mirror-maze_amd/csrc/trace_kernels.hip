@@ -291,10 +291,12 @@ __device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
 // The record (TileJob::ring_diag, host-mapped, 16 words; mm_last_error prints
 // it): [0] 1 = written, [1] role (1 reader, 2 writer), [2] entry seq, [3]
 // wanted turn value, [4] the turn value last seen, [5] reserved, [6] claimed,
-// [7] block, [8] wave, [9] lane, [10..11] wall clock at the wait's first
-// failed poll, [12..13] at the timeout (100 MHz), [14] polls, [15] launch id.
-__device__ __noinline__ void ring_timeout(const TileJob& job, uint32_t* err, uint32_t role, uint32_t seq,
-                                          uint32_t want, uint32_t seen, uint64_t t0, uint32_t polls) {
+// [7] block, [8] wave, [9] lane, [10..11] 0, [12..13] wall clock at the
+// timeout (100 MHz), [14] polls, [15] launch id.  (No clock at the wait's
+// start: a 64-bit value live across the wait loop cost the deferral kernel
+// 10 more scratch operations in its chunk loop; the polls give the length.)
+__device__ __forceinline__ void ring_timeout(const TileJob& job, uint32_t* err, uint32_t role, uint32_t seq,
+                                             uint32_t want, uint32_t seen, uint32_t polls) {
     if (atomicOr(err, kErrRing) & kErrRing) return;  // not the launch's first timeout
     uint32_t* d = job.ring_diag;
     if (!d) return;
@@ -302,7 +304,7 @@ __device__ __noinline__ void ring_timeout(const TileJob& job, uint32_t* err, uin
     d[1] = role; d[2] = seq; d[3] = want; d[4] = seen;
     d[5] = lds_ld(ring_ctl() + 0); d[6] = lds_ld(ring_ctl() + 1);
     d[7] = blockIdx.x; d[8] = threadIdx.x >> 6; d[9] = threadIdx.x & 63u;
-    d[10] = (uint32_t)t0; d[11] = (uint32_t)(t0 >> 32); d[12] = (uint32_t)t1; d[13] = (uint32_t)(t1 >> 32);
+    d[10] = 0u; d[11] = 0u; d[12] = (uint32_t)t1; d[13] = (uint32_t)(t1 >> 32);
     d[14] = polls; d[15] = job.launch_id;
     __threadfence_system();
     __hip_atomic_store(d, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -311,13 +313,11 @@ __device__ __noinline__ void ring_timeout(const TileJob& job, uint32_t* err, uin
 __device__ __forceinline__ bool ring_wait(uint32_t seq, uint32_t c, uint32_t role, const TileJob& job, uint32_t* err) {
     uint32_t* turn = ring_turn(seq);
     const uint32_t want = ring_turn_value(seq, c);
-    uint64_t t0 = 0;
     for (uint32_t i = 0;; ++i) {
         const uint32_t seen = lds_ld(turn);
         if (seen == want) return true;
-        if (i == 0) t0 = wall_clock64();
         if (i >= job.ring_spin) {
-            ring_timeout(job, err, role, seq, want, seen, t0, i);
+            ring_timeout(job, err, role, seq, want, seen, i);
             return false;
         }
         __builtin_amdgcn_s_sleep(1);

@@ -254,6 +254,7 @@ static inline void consider(float a, uint32_t k, float* best, uint32_t* bk, int*
 #define MAXC 128
 static __thread int q_len[MAXC];   /* list lengths of the cells the last query visited */
 static __thread int q_n;
+static __thread int q_cell0, q_oct;  /* the last query's start cell and direction octant (DUMP) */
 /* crossing time of boundary b along axis a: the kernel's fma form (mm_grid.h,
  * default) or, with DIRECT=1, the direct form ((mn + b cell) - o) * y */
 static float cell_time(int a, int b, float o, float y) {
@@ -288,6 +289,8 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
     }
     int ncell = 0;
     q_n = 0;
+    q_cell0 = (ic[2] * gn[1] + ic[1]) * gn[0] + ic[0];
+    q_oct = (dd[0] > 0.0f) | ((dd[1] > 0.0f) << 1) | ((dd[2] > 0.0f) << 2);
     uint32_t seen[256]; int n_seen = 0; long prev_c = -1; int face = -1;
     for (;;) {
         long c = ((long)ic[2] * gn[1] + ic[1]) * gn[0] + ic[0];
@@ -342,6 +345,25 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
 /* wave model: per lane, per bounce, the list lengths of the visited cells */
 #define MAXB 32
 static __thread int w_len[64][MAXB][16], w_n[64][MAXB], w_nb[64], w_lane;
+/* DUMP=<file>: one 16-byte record per query, in path order, for the regrouping
+   model (scripts/regroup_model.cpp): path id, bounce, start cell, octant, cells
+   visited, the list length of the first 8 cells, and the rejection-sampling
+   trials of the shading that follows (0: mirror bounce or path end). */
+typedef struct {
+    uint32_t path;
+    uint16_t cell0;
+    uint8_t bounce, oct, ncells, trials, lens[6];
+} qrec_t;
+static FILE* dump_f;
+static __thread qrec_t* dump_buf;
+static __thread size_t dump_n, dump_cap;
+static __thread uint32_t dump_path;
+static void dump_flush(void) {
+    if (!dump_n) return;
+#pragma omp critical(dump)
+    fwrite(dump_buf, sizeof(qrec_t), dump_n, dump_f);
+    dump_n = 0;
+}
 /* the reference path loop with every query cross-checked */
 static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t* tr, uint64_t* rays) {
     ray_t b;
@@ -355,6 +377,14 @@ static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t
         st->queries++;
         const uint64_t t_before = st->tests, c_before = st->cells;
         int ok_q = grid_query(b.ori, b.dir, &gt, &gi, st);
+        qrec_t* qr = NULL;
+        if (dump_f) {
+            if (dump_n == dump_cap) { dump_cap = dump_cap ? 2 * dump_cap : 1 << 16; dump_buf = realloc(dump_buf, dump_cap * sizeof(qrec_t)); }
+            qr = &dump_buf[dump_n++];
+            qr->path = dump_path; qr->cell0 = (uint16_t)q_cell0; qr->bounce = (uint8_t)n; qr->oct = (uint8_t)q_oct;
+            qr->ncells = (uint8_t)(q_n < 255 ? q_n : 255); qr->trials = 0;
+            for (int c = 0; c < 6; ++c) qr->lens[c] = (uint8_t)(c < q_n ? (q_len[c] < 255 ? q_len[c] : 255) : 0);
+        }
         if (n >= bl) { st->tail_q++; st->tail_tests += st->tests - t_before; st->tail_cells += st->cells - c_before; }
         if (n < MAXB) {
             w_n[w_lane][n] = q_n < 16 ? q_n : 16;
@@ -382,11 +412,14 @@ static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t
             float rx = oracle_rand_pm1(&seed), ry = oracle_rand_pm1(&seed), rz = oracle_rand_pm1(&seed);
             v3 rd = mk(rx, ry, rz);
             float len2 = dot3(rd, rd);
+            int trials = 1;
             while (sqrtf(len2) > 1.0f) {
                 rx = oracle_rand_pm1(&seed); ry = oracle_rand_pm1(&seed); rz = oracle_rand_pm1(&seed);
                 rd = mk(rx, ry, rz);
                 len2 = dot3(rd, rd);
+                trials++;
             }
+            if (qr) qr->trials = (uint8_t)(trials < 255 ? trials : 255);
             v3 rn = vscale(rsq(len2), rd);
             b.ori = vadd(b.ori, vscale(b.t, b.dir));
             v3 nd = vadd(rn, vscale(side, nn));
@@ -415,6 +448,7 @@ int main(int argc, char** argv) {
     int W = atoi(argv[2]), H = atoi(argv[3]), spp = atoi(argv[4]), bl = atoi(argv[5]), ml = atoi(argv[6]);
     int rs = atoi(argv[7]);
     build_grid(argc > 8 ? atof(argv[8]) : 0.0);
+    if (getenv("DUMP")) dump_f = fopen(getenv("DUMP"), "wb");
     build_faces();
     mm_uniform u;
     /* default camera (mm_uniform_default): centre (-5,0,-45), quat from (0.1,0,1), focal 1, viewport (2W/H, 2) */
@@ -442,11 +476,13 @@ int main(int argc, char** argv) {
                     int x = x0 + l / spp, k = l % spp;
                     w_lane = l; w_nb[l] = 0;
                     if (x >= W) continue;
+                    dump_path = (uint32_t)(((uint64_t)y * W + x) * spp + k);
                     v3 d0 = primary_dir(&u, x, y);
                     uint32_t seed = oracle_tile_seed(y * W + x, k, 0);
                     v3 d = jittered_dir(d0, &seed);
                     path(ld3(u.cam.center), d, seed, bl, ml, &st, &tr, &rays);
                 }
+                if (dump_f && dump_n > (1u << 22)) dump_flush();  /* (between chunks: a path's records stay together) */
                 { int mx = 0, sum = 0, cnt = 0;
                   for (int l = 0; l < 64; ++l) if (w_nb[l] > 0) { sum += w_nb[l]; cnt++; if (w_nb[l] > mx) mx = w_nb[l]; }
                   if (cnt) { nbmax += mx; nbsum += (double)sum / cnt; nbw++;
@@ -501,6 +537,7 @@ int main(int argc, char** argv) {
                     cont[K] += cost;
                 }
             }
+        if (dump_f) dump_flush();
 #pragma omp critical
         { wnest += nest + lockS; wflat += flat + lockS; wtest += ntest; wstep += nstep; wshade += lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K];
           gnbmax += nbmax; gnbsum += nbsum; gnbw += nbw; for (int b = 0; b < 32; ++b) { gact[b] += act_hist[b]; git[b] += it_hist[b]; } }
