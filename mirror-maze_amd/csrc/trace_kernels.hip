@@ -161,21 +161,54 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // resolved by k_resolve (the same operations in the same order as the fused
 // resolve).
 
-// A deferred path's state into / out of queue record i (mm_launch.h TailQueue).
-__device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t i, const PathState& p, uint32_t slot) {
-    uint4* r = q.rec + 4u * (size_t)i;
-    r[0] = make_uint4(__float_as_uint(p.ori.x), __float_as_uint(p.ori.y), __float_as_uint(p.ori.z),
-                      __float_as_uint(p.dir.x));
-    r[1] = make_uint4(__float_as_uint(p.dir.y), __float_as_uint(p.dir.z), __float_as_uint(p.T.x),
-                      __float_as_uint(p.T.y));
-    r[2] = make_uint4(__float_as_uint(p.T.z), __float_as_uint(p.L.x), __float_as_uint(p.L.y),
-                      __float_as_uint(p.L.z));
-    r[3] = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, 0u);
+// A deferred path's state (64 B: ori.xyz dir.x | dir.yz T.xy | T.z L.xyz |
+// seed, n | mh << 16, sample slot, 0) into / out of slot s of block b's tail
+// ring.  MM_RING_LDS (default): the payload lives in the block's LDS beside
+// the turn words, word group j of slot s at ring_pay()[j * kTailRing + s] (a
+// wave's consecutive entries are consecutive 16-B words: no bank conflicts),
+// 32 KB per block; the deferral kernel then runs only where the grid image
+// leaves room (mm_runtime.hip: C3's 44 KB image + 34 KB static LDS per block,
+// two blocks per CU).  Otherwise: the queue's global records b * kTailRing + s
+// (mm_launch.h TailQueue).
+#ifndef MM_RING_LDS
+#define MM_RING_LDS 1
+#endif
+__device__ __forceinline__ uint4* ring_pay() {
+#if MM_RING_LDS
+    __shared__ uint4 pay[4 * kTailRing];
+    return pay;
+#else
+    return nullptr;
+#endif
 }
 
-__device__ __forceinline__ uint32_t tail_load(const TailQueue& q, uint32_t i, PathState& p) {
-    const uint4* r = q.rec + 4u * (size_t)i;
+__device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t s, const PathState& p, uint32_t slot) {
+    const uint4 w0 = make_uint4(__float_as_uint(p.ori.x), __float_as_uint(p.ori.y), __float_as_uint(p.ori.z),
+                                __float_as_uint(p.dir.x));
+    const uint4 w1 = make_uint4(__float_as_uint(p.dir.y), __float_as_uint(p.dir.z), __float_as_uint(p.T.x),
+                                __float_as_uint(p.T.y));
+    const uint4 w2 = make_uint4(__float_as_uint(p.T.z), __float_as_uint(p.L.x), __float_as_uint(p.L.y),
+                                __float_as_uint(p.L.z));
+    const uint4 w3 = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, 0u);
+#if MM_RING_LDS
+    (void)q;
+    uint4* r = ring_pay() + s;
+    r[0] = w0; r[kTailRing] = w1; r[2 * kTailRing] = w2; r[3 * kTailRing] = w3;
+#else
+    uint4* r = q.rec + 4u * ((size_t)blockIdx.x * kTailRing + s);
+    r[0] = w0; r[1] = w1; r[2] = w2; r[3] = w3;
+#endif
+}
+
+__device__ __forceinline__ uint32_t tail_load(const TailQueue& q, uint32_t s, PathState& p) {
+#if MM_RING_LDS
+    (void)q;
+    const uint4* r = ring_pay() + s;
+    const uint4 a = r[0], b = r[kTailRing], c = r[2 * kTailRing], d = r[3 * kTailRing];
+#else
+    const uint4* r = q.rec + 4u * ((size_t)blockIdx.x * kTailRing + s);
     const uint4 a = r[0], b = r[1], c = r[2], d = r[3];
+#endif
     p.ori = F3{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
     p.dir = F3{__uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)};
     p.T = F3{__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x)};
@@ -209,15 +242,18 @@ __device__ __forceinline__ F3 path_value(const PathState& p) {
 // payload, no L2 writeback or invalidate.  Protocol model:
 // tests/ring_model/ring_model.cpp (tests/test_ring_model.py).
 //
-// Memory ordering of the payload: the release of a turn
-// word is a plain ds_write_b32 with no s_waitcnt vmcnt before it -- the
-// writer's four global_store_dwordx4 and the reader's four
-// global_load_dwordx4 are still in flight when it issues (DESIGN.md s4 quotes
-// the ISA).  That is LLVM's AMDGPU memory model for a workgroup-scope release
-// on gfx94x/gfx950 outside threadgroup-split mode (.amdhsa_tg_split 0 here):
-// all waves of a work-group use the same vector L1, which serves a CU's
-// vector memory requests in order, so a later load by a block-mate that has
-// seen the turn word cannot pass the earlier stores; no wait is needed.
+// Memory ordering of the payload.  Payload in LDS
+// (MM_RING_LDS): payload and turn word are both LDS operations of the same
+// wave, and the workgroup-scope release / acquire put s_waitcnt lgkmcnt(0)
+// between them.  Payload in global memory: the release of a turn word is a
+// plain ds_write_b32 with no s_waitcnt vmcnt before it -- the writer's four
+// global_store_dwordx4 and the reader's four global_load_dwordx4 are still in
+// flight when it issues (DESIGN.md s4 quotes the ISA).  That is LLVM's AMDGPU
+// memory model for a workgroup-scope release on gfx94x/gfx950 outside
+// threadgroup-split mode (.amdhsa_tg_split 0 here): all waves of a work-group
+// use the same vector L1, which serves a CU's vector memory requests in
+// order, so a later load by a block-mate that has seen the turn word cannot
+// pass the earlier stores; no wait is needed.
 __device__ __forceinline__ uint32_t* ring_ctl() {
     __shared__ uint32_t words[4 + kTailRing];
     return words;
@@ -342,8 +378,23 @@ constexpr uint32_t kClaimChunks = MM_CLAIM_CHUNKS;  // chunks per dequeue (A/B: 
 // The wave's claimed range [next, end) lives in LDS, not in registers held
 // across the bounce loop (SGPR pressure there spills into VGPR lanes).
 __device__ __forceinline__ uint32_t* claim_words() {
-    __shared__ uint32_t w[2 * 16];  // (next, end) per wave of a <= 1024-thread block
-    return w + 2 * (threadIdx.x >> 6);
+    // (next, end) per wave of a <= 1024-thread block, then (diagnostics, job.wave_ts) the wall clock at the
+    // start of the wave's current chunk
+    __shared__ uint32_t w[4 * 16];
+    return w + 4 * (threadIdx.x >> 6);
+}
+// Diagnostics build -DMM_TAIL_CLOCKS (mm_set_wave_timeline): the start of the wave's current chunk, for the
+// launch-tail probe (scripts/timeline_probe.py --tail: the last chunk's duration per wave, by XCD).
+__device__ __forceinline__ void mark_chunk_start(const TileJob& job) {
+#ifndef MM_TAIL_CLOCKS
+    (void)job;
+#else
+    if (job.wave_ts && (threadIdx.x & 63u) == 0) {
+        const uint64_t t = wall_clock64();
+        claim_words()[2] = (uint32_t)t;
+        claim_words()[3] = (uint32_t)(t >> 32);
+    }
+#endif
 }
 __device__ __forceinline__ void claim_reset() {
     if ((threadIdx.x & 63u) == 0) { claim_words()[0] = 0u; claim_words()[1] = 0u; }
@@ -382,6 +433,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
         const uint32_t base = dequeue(work, n_queue);
         if (base >= n_queue) break;
         ++chunks;
+        mark_chunk_start(job);
         const uint32_t qc = base >> 6;
         const uint32_t fr = job.n_frames > 1 ? qc / cpf : 0u;
         const uint32_t path = (qc - fr * cpf) * 64u + lane;
@@ -488,16 +540,16 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             }
         }
         ++chunks;
-        PathState p;
+        mark_chunk_start(job);
+        PathState p{};
         uint32_t slot = 0;
         bool live;
         if (k) {  // queued tails
             live = lane < k;
             if (live) {
                 const uint32_t seq = __builtin_amdgcn_readfirstlane(first) + lane;
-                const uint32_t rec = blockIdx.x * kTailRing + seq % kTailRing;
                 if (ring_wait(seq, 1u, 1u, job, err)) {
-                    slot = tail_load(tq, rec, p);
+                    slot = tail_load(tq, seq % kTailRing, p);
                     __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 2u), __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {  // the record was never written (its sample slot is unknown here: ADVICE r03): skip it;
@@ -538,7 +590,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             if (overflow) atomicOr(err, kErrStack);
             if (deferred) {
                 if (ring_wait(seq, 0u, 2u, job, err)) {
-                    tail_store(tq, blockIdx.x * kTailRing + seq % kTailRing, p, slot);
+                    tail_store(tq, seq % kTailRing, p, slot);
                     __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 1u), __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {
@@ -674,6 +726,9 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
     }
 }
 
+// Timeline records (mm_set_wave_timeline): wave wid's (entry, staged, exit, chunks) at 4 * wid, its (last
+// chunk start, XCC id, HW_ID, chunks) at 4 * (wid + kTimelineWaves) when the buffer holds them.
+[[maybe_unused]] constexpr uint32_t kTimelineWaves = 32768;
 // Per-wave diagnostics record and the self-cleaning counter pair shared by the
 // persistent kernels (counter[0] = next item, counter[1] = waves done; the
 // last wave to finish re-zeroes the words, so the next launch needs no memset
@@ -696,6 +751,21 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
 #endif
         }
     }
+#ifdef MM_TAIL_CLOCKS
+    if (job.wave_ts && (threadIdx.x & 63u) == 0) {
+        // second record per wave (index wid + kTimelineWaves): its last chunk's start, and where it ran:
+        // HW_REG_XCC_ID (the XCD, 0-7) and HW_REG_HW_ID (CU, SIMD, shader engine; MI355X_MICROARCH.md)
+        const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) + kTimelineWaves;
+        if (wid < job.wave_ts_cap) {
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);   // hwreg(HW_REG_XCC_ID, 0, 4)
+            const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // hwreg(HW_REG_HW_ID, 0, 32)
+            job.wave_ts[4 * wid + 0] = claim_words()[2] | (unsigned long long)claim_words()[3] << 32;
+            job.wave_ts[4 * wid + 1] = xcc;
+            job.wave_ts[4 * wid + 2] = hwid;
+            job.wave_ts[4 * wid + 3] = chunks;
+        }
+    }
+#endif
     if ((threadIdx.x & 63u) == 0) {
         __threadfence();
         const uint32_t total = gridDim.x * (blockDim.x >> 6);
@@ -800,7 +870,7 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     const uint32_t grid =
         persistent_grid(kern, lds, job.reserve_cus, (uint64_t)job.w * job.h * job.e.spp * job.n_frames);
     if (!grid) return hipErrorInvalidValue;
-    if (kDefer && (uint64_t)grid * kTailRing > job.tail.cap) return hipErrorInvalidValue;
+    if (kDefer && !MM_RING_LDS && (uint64_t)grid * kTailRing > job.tail.cap) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWpThreads), lds, s, sc, job, samples, stats, err, work);
     return hipGetLastError();
 }

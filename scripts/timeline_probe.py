@@ -16,6 +16,39 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "mirror-maze_amd"))
 
 
+TIMELINE_WAVES = 32768  # trace_kernels.hip kTimelineWaves: the second record of wave w is at w + 32768
+
+
+def tail_report(raw, t0, np):
+    """Launch tail by XCD and by the last chunk (MM_TAIL_CLOCKS build): for each
+    wave, exit time, XCD, and the start of its last chunk."""
+    n = TIMELINE_WAVES
+    wid = np.nonzero(raw[:n, 2] > 0)[0]
+    ext = (raw[wid, 2] - t0) / 100.0
+    last = raw[n + wid, 0]
+    ok = last > 0
+    xcc = raw[n + wid, 1]
+    dur = np.where(ok, (raw[wid, 2] - last) / 100.0, np.nan)
+    span = ext.max()
+    first_out = ext.min()
+    print(f"    tail {span - first_out:.1f} us; last chunk duration p50 {np.nanmedian(dur):.1f} p90 "
+          f"{np.nanpercentile(dur, 90):.1f} max {np.nanmax(dur):.1f} us", flush=True)
+    for x in sorted(set(xcc.tolist())):
+        m = xcc == x
+        e = ext[m]
+        print(f"    XCD {x}: {m.sum():5d} waves, exit min/p50/p90/max {e.min():7.1f}/{np.median(e):7.1f}/"
+              f"{np.percentile(e, 90):7.1f}/{e.max():7.1f}, last chunk p50/max {np.nanmedian(dur[m]):6.1f}/"
+              f"{np.nanmax(dur[m]):6.1f}", flush=True)
+    # the last 2 % of exits: were they waves with a long last chunk, or late starters?
+    k = max(1, len(ext) // 50)
+    idx = np.argsort(ext)[-k:]
+    lstart = np.where(ok, (last - t0) / 100.0, np.nan)
+    print(f"    last {k} waves out: exit {ext[idx].min():.1f}..{ext[idx].max():.1f}, last chunk started "
+          f"p50 {np.nanmedian(lstart[idx]):.1f} (queue empty ~{first_out:.1f}), lasted p50 {np.nanmedian(dur[idx]):.1f} "
+          f"max {np.nanmax(dur[idx]):.1f} us; XCDs {np.bincount(xcc[idx].astype(int), minlength=8).tolist()}",
+          flush=True)
+
+
 def main():
     import numpy as np
     import torch
@@ -30,6 +63,9 @@ def main():
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--opt", action="append", default=[], help="MM_OPT key:value (repeatable)")
     ap.add_argument("--batch", type=int, default=1, help="frames per launch (mm_trace_tile_frames), as bench.py")
+    ap.add_argument("--tail", action="store_true",
+                    help="attribute the launch tail (needs a -DMM_TAIL_CLOCKS build via MIRROR_MAZE_LIB): per XCD "
+                         "(HW_REG_XCC_ID) exit times, and each wave's last chunk duration")
     a = ap.parse_args()
     maze_n, W, H, spp, bl, ml, desc = CONFIGS[a.config]
     r = Renderer(0)
@@ -76,6 +112,8 @@ def main():
             bmean = np.array([ext[blk == b].mean() for b in np.unique(blk)])
             print(f"    block-balanced bound: last block mean exit {bmean.max():7.1f} (vs last wave {span:7.1f}); "
                   f"chip mean exit {ext.mean():7.1f}", flush=True)
+            if a.tail:
+                tail_report(ts.cpu().numpy(), t0, np)
     r.close()
 
 
