@@ -60,6 +60,8 @@ struct TileJob {
     // defer_from >= 2^30: off.
     uint32_t defer_from = 1u << 30, defer_lanes = 0;
     TailQueue tail;
+    // 1: the rings' records in LDS (the kRing = 2 kernel, where the grid image leaves room); 0: in `tail`
+    uint32_t ring_lds = 0;
     // Per-launch status word (host-mapped pinned memory, mm_runtime.hip): the
     // last wave of the launch moves the error flag into it, | kStatusDone, so
     // the host attributes an error to the call that launched it without a
@@ -113,7 +115,8 @@ size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
 bool wavepersist_defer_built(int lds_mode, int form);
 bool wavepersist_built(int lds_mode, int form);
 // Register / scratch / LDS use of the (kStats = false) instance.
-hipError_t wavepersist_attributes(int lds_mode, int form, bool defer, hipFuncAttributes* a);
+// ring: 0 no tail deferral, 1 rings with global records, 2 rings with records in LDS.
+hipError_t wavepersist_attributes(int lds_mode, int form, int ring, hipFuncAttributes* a);
 // Built with -DMM_AB_VARIANTS (the A/B-only placements and k_trace_mega's
 // non-reference forms).
 bool ab_variants_built();

@@ -123,7 +123,7 @@ struct mm_ctx {
     bool opt_grid_wide = true;   // MM_OPT_GRID_WIDE (read by mm_upload_scene)
     bool last_defer = false;     // the last trace call ran the tail rings
     int last_kern_mode = -1, last_kern_form = -1;  // for MM_INFO_LAST_VGPRS / _SCRATCH
-    bool last_kern_defer = false;
+    int last_kern_ring = 0;      // its tail-ring kind (wavepersist_attributes: 0 none, 1 global, 2 LDS records)
 };
 
 constexpr uint32_t kStatusSlots = 1024;
@@ -553,7 +553,7 @@ int mm_scene_info(const mm_ctx* c, int key, double* value) {
         case MM_INFO_LAST_STATIC_LDS: {
             if (c->last_kern_mode < 0) return MM_ERR_INVALID;
             hipFuncAttributes a{};
-            if (wavepersist_attributes(c->last_kern_mode, c->last_kern_form, c->last_kern_defer, &a) != hipSuccess)
+            if (wavepersist_attributes(c->last_kern_mode, c->last_kern_form, c->last_kern_ring, &a) != hipSuccess)
                 return MM_ERR_HIP;
             *value = key == MM_INFO_LAST_VGPRS ? a.numRegs
                      : key == MM_INFO_LAST_SCRATCH ? (double)a.localSizeBytes : (double)a.sharedSizeBytes;
@@ -967,15 +967,26 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                            "method / LDS placement (grid search, or BVH form 7 with nodes + "
                                            "records in LDS)");
     bool defer = defer_built && (defer_on || wave) && (wave || tile_paths * n_frames >= c->opt_defer_min);
-    // the deferral kernel's static LDS (tail ring, claimed queue ranges) must leave two 1024-thread blocks per
-    // CU: a grid image within that of the 80 KB budget runs without the rings
-    hipFuncAttributes dattr{};
-    const size_t defer_static = (defer && wavepersist_attributes(mode, form, true, &dattr) == hipSuccess)
-                                    ? dattr.sharedSizeBytes
-                                    : (4 + kTailRing) * sizeof(uint32_t) + 128;
-    if (defer && wavepersist_lds_bytes(sc, mode) + defer_static > 80 * 1024) {
-        if (wave) return fail(c, MM_ERR_UNSUPPORTED, "MM_PIPE_WAVEFRONT: grid image + tail ring exceed the LDS budget");
-        defer = false;
+    // the deferral kernel's static LDS (tail ring, claimed queue ranges, and with ring kind 2 the rings'
+    // 32 KB of records) must leave two 1024-thread blocks per CU: the records go to LDS where the
+    // image leaves room (C3: 44 KB + 34 KB), else to global memory; a grid image without room even for the
+    // ring words runs without the rings
+    int ring = 0;
+    if (defer) {
+        const size_t img = wavepersist_lds_bytes(sc, mode);
+        for (int kind : {2, 1}) {
+            hipFuncAttributes dattr{};
+            if (wavepersist_attributes(mode, form, kind, &dattr) == hipSuccess &&
+                img + dattr.sharedSizeBytes <= 80 * 1024) {
+                ring = kind;
+                break;
+            }
+        }
+        if (!ring) {
+            if (wave)
+                return fail(c, MM_ERR_UNSUPPORTED, "MM_PIPE_WAVEFRONT: grid image + tail ring exceed the LDS budget");
+            defer = false;
+        }
     }
     const bool fusable = persist && c->opt_fuse && 64 % e->spp == 0;
     // staging bound: a multi-frame launch stages all its frames at once; past kStagePathsMax it runs without
@@ -1010,7 +1021,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                                    (size_t)(row_paths * rows_per_batch) * (defer ? n_frames : 1));
     if (rc) return rc;
     TailQueue tq;
-    if (defer && (rc = tail_queue(c, tq))) return rc;
+    if (defer && ring == 1 && (rc = tail_queue(c, tq))) return rc;  // (records in LDS: no global ring)
     // aux: [0..3] stats (zeroed only when counted), [4] error flag (moved into the launch's status word by
     // the launch itself), [5] lane-refill counter (zeroed by its launcher), [6] wave-persistent counter pair
     // (self-cleaning).  No fill kernel on the default path: see k_trace_wavepersist.
@@ -1041,6 +1052,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             job.defer_from = 1;
             job.defer_lanes = c->opt_defer > 0 ? (uint32_t)c->opt_defer : 32u;
             job.tail = tq;
+            job.ring_lds = ring == 2 ? 1u : 0u;
         }
         // The launch's status slot is taken first (its device address is a kernel argument); if the
         // launch then fails to enqueue, the slot is released as finished-clean (a slot left
@@ -1059,7 +1071,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                 c->last_mode = mode;
                 c->last_kern_mode = mode;
                 c->last_kern_form = form;
-                c->last_kern_defer = defer;
+                c->last_kern_ring = defer ? ring : 0;
                 HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux, err_dev,
                                                  reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
                                                  c->stream));

@@ -162,26 +162,20 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // resolve).
 
 // A deferred path's state (64 B: ori.xyz dir.x | dir.yz T.xy | T.z L.xyz |
-// seed, n | mh << 16, sample slot, 0) into / out of slot s of block b's tail
-// ring.  MM_RING_LDS (default): the payload lives in the block's LDS beside
-// the turn words, word group j of slot s at ring_pay()[j * kTailRing + s] (a
-// wave's consecutive entries are consecutive 16-B words: no bank conflicts),
-// 32 KB per block; the deferral kernel then runs only where the grid image
-// leaves room (mm_runtime.hip: C3's 44 KB image + 34 KB static LDS per block,
-// two blocks per CU).  Otherwise: the queue's global records b * kTailRing + s
-// (mm_launch.h TailQueue).
-#ifndef MM_RING_LDS
-#define MM_RING_LDS 1
-#endif
+// seed, n | mh << 16, sample slot, 0) into / out of slot s of its block's tail
+// ring.  kLdsPay (the deferral kernel with kRing = 2, chosen where the grid
+// image leaves room -- C3: 44 KB image + 34 KB static LDS per block, two
+// blocks per CU): the payload lives in the block's LDS beside the turn words,
+// word group j of slot s at ring_pay()[j * kTailRing + s] (a wave's
+// consecutive entries are consecutive 16-B words: no bank conflicts), 32 KB
+// per block.  Otherwise (kRing = 1): the queue's global records
+// blockIdx.x * kTailRing + s (mm_launch.h TailQueue).
 __device__ __forceinline__ uint4* ring_pay() {
-#if MM_RING_LDS
     __shared__ uint4 pay[4 * kTailRing];
     return pay;
-#else
-    return nullptr;
-#endif
 }
 
+template <bool kLdsPay>
 __device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t s, const PathState& p, uint32_t slot) {
     const uint4 w0 = make_uint4(__float_as_uint(p.ori.x), __float_as_uint(p.ori.y), __float_as_uint(p.ori.z),
                                 __float_as_uint(p.dir.x));
@@ -190,25 +184,25 @@ __device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t s, const
     const uint4 w2 = make_uint4(__float_as_uint(p.T.z), __float_as_uint(p.L.x), __float_as_uint(p.L.y),
                                 __float_as_uint(p.L.z));
     const uint4 w3 = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, 0u);
-#if MM_RING_LDS
-    (void)q;
-    uint4* r = ring_pay() + s;
-    r[0] = w0; r[kTailRing] = w1; r[2 * kTailRing] = w2; r[3 * kTailRing] = w3;
-#else
-    uint4* r = q.rec + 4u * ((size_t)blockIdx.x * kTailRing + s);
-    r[0] = w0; r[1] = w1; r[2] = w2; r[3] = w3;
-#endif
+    if constexpr (kLdsPay) {
+        uint4* r = ring_pay() + s;
+        r[0] = w0; r[kTailRing] = w1; r[2 * kTailRing] = w2; r[3 * kTailRing] = w3;
+    } else {
+        uint4* r = q.rec + 4u * ((size_t)blockIdx.x * kTailRing + s);
+        r[0] = w0; r[1] = w1; r[2] = w2; r[3] = w3;
+    }
 }
 
+template <bool kLdsPay>
 __device__ __forceinline__ uint32_t tail_load(const TailQueue& q, uint32_t s, PathState& p) {
-#if MM_RING_LDS
-    (void)q;
-    const uint4* r = ring_pay() + s;
-    const uint4 a = r[0], b = r[kTailRing], c = r[2 * kTailRing], d = r[3 * kTailRing];
-#else
-    const uint4* r = q.rec + 4u * ((size_t)blockIdx.x * kTailRing + s);
-    const uint4 a = r[0], b = r[1], c = r[2], d = r[3];
-#endif
+    uint4 a, b, c, d;
+    if constexpr (kLdsPay) {
+        const uint4* r = ring_pay() + s;
+        a = r[0]; b = r[kTailRing]; c = r[2 * kTailRing]; d = r[3 * kTailRing];
+    } else {
+        const uint4* r = q.rec + 4u * ((size_t)blockIdx.x * kTailRing + s);
+        a = r[0]; b = r[1]; c = r[2]; d = r[3];
+    }
     p.ori = F3{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
     p.dir = F3{__uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)};
     p.T = F3{__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x)};
@@ -243,7 +237,7 @@ __device__ __forceinline__ F3 path_value(const PathState& p) {
 // tests/ring_model/ring_model.cpp (tests/test_ring_model.py).
 //
 // Memory ordering of the payload.  Payload in LDS
-// (MM_RING_LDS): payload and turn word are both LDS operations of the same
+// (kRing = 2): payload and turn word are both LDS operations of the same
 // wave, and the workgroup-scope release / acquire put s_waitcnt lgkmcnt(0)
 // between them.  Payload in global memory: the release of a turn word is a
 // plain ds_write_b32 with no s_waitcnt vmcnt before it -- the writer's four
@@ -377,27 +371,52 @@ constexpr uint32_t kClaimChunks = MM_CLAIM_CHUNKS;  // chunks per dequeue (A/B: 
 // chunk per claim (259,200 chunks in 2.95 ms; profiles/r03/ab_claim_chunks.txt).
 // The wave's claimed range [next, end) lives in LDS, not in registers held
 // across the bounce loop (SGPR pressure there spills into VGPR lanes).
+#ifdef MM_TAIL_CLOCKS
+constexpr uint32_t kClaimWords = 8;
+#else
+constexpr uint32_t kClaimWords = 2;
+#endif
 __device__ __forceinline__ uint32_t* claim_words() {
-    // (next, end) per wave of a <= 1024-thread block, then (diagnostics, job.wave_ts) the wall clock at the
-    // start of the wave's current chunk
-    __shared__ uint32_t w[4 * 16];
-    return w + 4 * (threadIdx.x >> 6);
+    // (next, end) per wave of a <= 1024-thread block; diagnostics build MM_TAIL_CLOCKS: then the wall clock at
+    // the start of the wave's current chunk (lo, hi), its longest chunk so far (10 ns units), its chunks over
+    // 100 us, the clock when it saw the global queue out (lo, hi)
+    __shared__ uint32_t w[kClaimWords * 16];
+    return w + kClaimWords * (threadIdx.x >> 6);
 }
-// Diagnostics build -DMM_TAIL_CLOCKS (mm_set_wave_timeline): the start of the wave's current chunk, for the
-// launch-tail probe (scripts/timeline_probe.py --tail: the last chunk's duration per wave, by XCD).
-__device__ __forceinline__ void mark_chunk_start(const TileJob& job) {
+// Diagnostics build -DMM_TAIL_CLOCKS (mm_set_wave_timeline), for the launch-tail probe
+// (scripts/timeline_probe.py --tail): chunk start times and durations per wave.  kind: 0 new, 1 tail.
+__device__ __forceinline__ void mark_chunk_start(const TileJob& job, uint32_t kind) {
+#ifndef MM_TAIL_CLOCKS
+    (void)job; (void)kind;
+#else
+    if (job.wave_ts && (threadIdx.x & 63u) == 0) {
+        uint32_t* cw = claim_words();
+        const uint64_t t = wall_clock64();
+        const uint64_t prev = cw[2] | (uint64_t)cw[3] << 32;
+        if (prev) {
+            const uint32_t d = (uint32_t)min<uint64_t>(t - prev, 0xFFFFFFFFull);
+            cw[4] = max(cw[4], d);
+            cw[5] += d > 10000u ? 1u : 0u;
+        }
+        cw[2] = (uint32_t)t;
+        cw[3] = (uint32_t)(t >> 32) | (kind << 31);
+    }
+#endif
+}
+__device__ __forceinline__ void mark_queue_out(const TileJob& job) {
 #ifndef MM_TAIL_CLOCKS
     (void)job;
 #else
-    if (job.wave_ts && (threadIdx.x & 63u) == 0) {
+    if (job.wave_ts && (threadIdx.x & 63u) == 0 && !claim_words()[7]) {
         const uint64_t t = wall_clock64();
-        claim_words()[2] = (uint32_t)t;
-        claim_words()[3] = (uint32_t)(t >> 32);
+        claim_words()[6] = (uint32_t)t;
+        claim_words()[7] = (uint32_t)(t >> 32);
     }
 #endif
 }
 __device__ __forceinline__ void claim_reset() {
-    if ((threadIdx.x & 63u) == 0) { claim_words()[0] = 0u; claim_words()[1] = 0u; }
+    if ((threadIdx.x & 63u) == 0)
+        for (uint32_t i = 0; i < kClaimWords; ++i) claim_words()[i] = 0u;
 }
 __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
     uint32_t* cw = claim_words();
@@ -431,9 +450,12 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     claim_reset();
     for (;;) {
         const uint32_t base = dequeue(work, n_queue);
-        if (base >= n_queue) break;
+        if (base >= n_queue) {
+            mark_queue_out(job);
+            break;
+        }
         ++chunks;
-        mark_chunk_start(job);
+        mark_chunk_start(job, 0u);
         const uint32_t qc = base >> 6;
         const uint32_t fr = job.n_frames > 1 ? qc / cpf : 0u;
         const uint32_t path = (qc - fr * cpf) * 64u + lane;
@@ -491,7 +513,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
 // last up to bounce_limit + mirror_limit iterations, would need a bound that a
 // valid 32767-bounce chunk outlasts).  A tail chunk runs the same bounce loop
 // as a new one (and may defer again) -- one copy of the loop in the kernel.
-template <bool kStats, typename Q>
+template <bool kStats, bool kLdsPay, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, const Q& q, const TileJob& job,
                                               float4* __restrict__ samples, unsigned long long* stats, uint32_t* err,
                                               uint32_t* work) {
@@ -536,11 +558,12 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             b = dequeue(work, n_queue);
             if (b >= n_queue) {
                 defer_from = 1 << 30;
+                mark_queue_out(job);
                 continue;
             }
         }
         ++chunks;
-        mark_chunk_start(job);
+        mark_chunk_start(job, k ? 1u : 0u);
         PathState p{};
         uint32_t slot = 0;
         bool live;
@@ -549,7 +572,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             if (live) {
                 const uint32_t seq = __builtin_amdgcn_readfirstlane(first) + lane;
                 if (ring_wait(seq, 1u, 1u, job, err)) {
-                    slot = tail_load(tq, seq % kTailRing, p);
+                    slot = tail_load<kLdsPay>(tq, seq % kTailRing, p);
                     __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 2u), __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {  // the record was never written (its sample slot is unknown here: ADVICE r03): skip it;
@@ -590,7 +613,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
             if (overflow) atomicOr(err, kErrStack);
             if (deferred) {
                 if (ring_wait(seq, 0u, 2u, job, err)) {
-                    tail_store(tq, seq % kTailRing, p, slot);
+                    tail_store<kLdsPay>(tq, seq % kTailRing, p, slot);
                     __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 1u), __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {
@@ -753,16 +776,24 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
     }
 #ifdef MM_TAIL_CLOCKS
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
-        // second record per wave (index wid + kTimelineWaves): its last chunk's start, and where it ran:
-        // HW_REG_XCC_ID (the XCD, 0-7) and HW_REG_HW_ID (CU, SIMD, shader engine; MI355X_MICROARCH.md)
+        // more records per wave (index wid + kTimelineWaves, wid + 2 kTimelineWaves): its last chunk's start
+        // (bit 63: a tail chunk), where it ran -- HW_REG_XCC_ID (the XCD, 0-7) and HW_REG_HW_ID (CU, SIMD,
+        // shader engine; MI355X_MICROARCH.md) --, chunks; its longest chunk (10 ns), chunks over 100 us, the
+        // clock when it saw the global queue out, the clock at its exit
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) + kTimelineWaves;
-        if (wid < job.wave_ts_cap) {
+        if (wid + kTimelineWaves < job.wave_ts_cap) {
+            const uint32_t* cw = claim_words();
             const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);   // hwreg(HW_REG_XCC_ID, 0, 4)
             const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // hwreg(HW_REG_HW_ID, 0, 32)
-            job.wave_ts[4 * wid + 0] = claim_words()[2] | (unsigned long long)claim_words()[3] << 32;
+            job.wave_ts[4 * wid + 0] = cw[2] | (unsigned long long)cw[3] << 32;
             job.wave_ts[4 * wid + 1] = xcc;
             job.wave_ts[4 * wid + 2] = hwid;
             job.wave_ts[4 * wid + 3] = chunks;
+            const uint32_t w2 = wid + kTimelineWaves;
+            job.wave_ts[4 * w2 + 0] = cw[4];
+            job.wave_ts[4 * w2 + 1] = cw[5];
+            job.wave_ts[4 * w2 + 2] = cw[6] | (unsigned long long)cw[7] << 32;
+            job.wave_ts[4 * w2 + 3] = (unsigned long long)wall_clock64();
         }
     }
 #endif
@@ -801,11 +832,12 @@ hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s)
 #define MM_WP_WAVES 8
 #endif
 constexpr uint32_t kWpThreads = MM_WP_THREADS;
-template <bool kStats, int kLds, int kForm, bool kDefer>
+// kRing: 0 no tail deferral; 1 tail rings, payload in global records; 2 tail rings, payload in LDS.
+template <bool kStats, int kLds, int kForm, int kRing>
 __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {
-    if constexpr (kDefer) {  // the block's tail ring: counters and turn words zero
+    if constexpr (kRing != 0) {  // the block's tail ring: counters and turn words zero
         for (uint32_t i = threadIdx.x; i < 4u + kTailRing; i += blockDim.x) ring_ctl()[i] = 0u;
         __syncthreads();
     }
@@ -820,8 +852,8 @@ __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersis
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
 #endif
     const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
-        if constexpr (kDefer)
-            return wavepersist_ring_body<kStats>(sc, q, job, samples, stats, err, work);
+        if constexpr (kRing != 0)
+            return wavepersist_ring_body<kStats, kRing == 2>(sc, q, job, samples, stats, err, work);
         else
             return wavepersist_body<kStats>(sc, q, job, samples, stats, err, work);
     });
@@ -860,17 +892,17 @@ static uint32_t persistent_grid(K kern, size_t lds, uint32_t reserve_cus, uint64
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, (items + kWpThreads - 1) / kWpThreads));
 }
 
-template <int kLds, int kForm, bool kDefer>
+template <int kLds, int kForm, int kRing>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        hipStream_t s) {
-    const size_t lds = wavepersist_lds_bytes(sc, kLds);  // (+ the tail ring's static LDS when kDefer)
-    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm, kDefer>
-                            : k_trace_wavepersist<false, kLds, kForm, kDefer>;
+    const size_t lds = wavepersist_lds_bytes(sc, kLds);  // (+ the tail ring's static LDS when kRing)
+    auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm, kRing>
+                            : k_trace_wavepersist<false, kLds, kForm, kRing>;
     const uint32_t grid =
         persistent_grid(kern, lds, job.reserve_cus, (uint64_t)job.w * job.h * job.e.spp * job.n_frames);
     if (!grid) return hipErrorInvalidValue;
-    if (kDefer && !MM_RING_LDS && (uint64_t)grid * kTailRing > job.tail.cap) return hipErrorInvalidValue;
+    if (kRing == 1 && (uint64_t)grid * kTailRing > job.tail.cap) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWpThreads), lds, s, sc, job, samples, stats, err, work);
     return hipGetLastError();
 }
@@ -922,29 +954,33 @@ bool wavepersist_defer_built(int lds_mode, int form) {
 hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s) {
-    const bool defer = job.defer_from < (1u << 30);
+    const int ring = job.defer_from < (1u << 30) ? (job.ring_lds ? 2 : 1) : 0;
 #define MM_WP(L, F)                                                                                          \
-    if (lds_mode == L && form == F && defer)                                                                 \
-        return launch_wavepersist_t<L, F, true>(sc, job, samples, stats, err, work, count_stats, s);
+    if (lds_mode == L && form == F && ring == 1)                                                             \
+        return launch_wavepersist_t<L, F, 1>(sc, job, samples, stats, err, work, count_stats, s);            \
+    if (lds_mode == L && form == F && ring == 2)                                                             \
+        return launch_wavepersist_t<L, F, 2>(sc, job, samples, stats, err, work, count_stats, s);
     MM_DEFER_INSTANCES(MM_WP)
 #undef MM_WP
 #define MM_WP(L, F)                                                                                          \
-    if (lds_mode == L && form == F && !defer)                                                                \
-        return launch_wavepersist_t<L, F, false>(sc, job, samples, stats, err, work, count_stats, s);
+    if (lds_mode == L && form == F && ring == 0)                                                             \
+        return launch_wavepersist_t<L, F, 0>(sc, job, samples, stats, err, work, count_stats, s);
     MM_WP_INSTANCES(MM_WP)
 #undef MM_WP
     return hipErrorInvalidValue;
 }
 
-hipError_t wavepersist_attributes(int lds_mode, int form, bool defer, hipFuncAttributes* a) {
+hipError_t wavepersist_attributes(int lds_mode, int form, int ring, hipFuncAttributes* a) {
 #define MM_WP(L, F)                                                                                          \
-    if (lds_mode == L && form == F && defer)                                                                 \
-        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, true>));
+    if (lds_mode == L && form == F && ring == 1)                                                             \
+        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, 1>));  \
+    if (lds_mode == L && form == F && ring == 2)                                                             \
+        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, 2>));
     MM_DEFER_INSTANCES(MM_WP)
 #undef MM_WP
 #define MM_WP(L, F)                                                                                          \
-    if (lds_mode == L && form == F && !defer)                                                                \
-        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, false>));
+    if (lds_mode == L && form == F && ring == 0)                                                             \
+        return hipFuncGetAttributes(a, reinterpret_cast<const void*>(k_trace_wavepersist<false, L, F, 0>));
     MM_WP_INSTANCES(MM_WP)
 #undef MM_WP
     return hipErrorInvalidValue;

@@ -2,14 +2,16 @@
 # rocprofv3 over bench.py's own launches (default issue mode: the timed frames in one multi-frame launch,
 # --steps 5 --warmup 0): one --kernel-trace --stats run, then one run per PMC counter set (--pmc never
 # combined with other traces), each under its own time limit.  Output: gpurun_out/<tag>/{stats,pmc1..5}.
-# Usage: bash scripts/pmc_bench.sh <tag> [config] [extra bench.py args, e.g. "--opt 21=0"]
+# Usage: [STEPS=20] bash scripts/pmc_bench.sh <tag> [config] [extra bench.py args, e.g. "--opt 21=0"]
+# (STEPS: the frames of the run -- bench.py puts up to 32 consecutive frames in one launch, so STEPS=20 profiles
+# the driver's own 20-frame C3 launch; default 5)
 set -o pipefail
-TAG=$1; CFG=${2:-c3}; XARGS=${3:-}
+TAG=$1; CFG=${2:-c3}; XARGS=${3:-}; STEPS=${STEPS:-5}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-B="$GRAFT_REPO_ROOT/bench.py --config $CFG --steps 5 --warmup 0 --no-cpu-baseline $XARGS"
+B="$GRAFT_REPO_ROOT/bench.py --config $CFG --steps $STEPS --warmup 0 --no-cpu-baseline $XARGS"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/stats -o run -- python3 $B > $OUT/stats.log 2>&1 \
   || { echo "stats run failed"; tail -5 $OUT/stats.log; exit 1; }
 i=0

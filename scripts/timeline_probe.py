@@ -20,33 +20,50 @@ TIMELINE_WAVES = 32768  # trace_kernels.hip kTimelineWaves: the second record of
 
 
 def tail_report(raw, t0, np):
-    """Launch tail by XCD and by the last chunk (MM_TAIL_CLOCKS build): for each
-    wave, exit time, XCD, and the start of its last chunk."""
+    """Launch tail (MM_TAIL_CLOCKS build): per wave its exit, XCD, last chunk
+    (start, new or tail), longest chunk, chunks over 100 us and the moment it
+    saw the global queue out."""
     n = TIMELINE_WAVES
     wid = np.nonzero(raw[:n, 2] > 0)[0]
     ext = (raw[wid, 2] - t0) / 100.0
-    last = raw[n + wid, 0]
+    r2, r3 = raw[n + wid], raw[2 * n + wid]
+    last_raw = r2[:, 0].astype(np.uint64)
+    is_tail = (last_raw >> np.uint64(63)).astype(bool)
+    last = (last_raw & np.uint64((1 << 63) - 1)).astype(np.int64)
     ok = last > 0
-    xcc = raw[n + wid, 1]
+    xcc = r2[:, 1]
     dur = np.where(ok, (raw[wid, 2] - last) / 100.0, np.nan)
-    span = ext.max()
-    first_out = ext.min()
-    print(f"    tail {span - first_out:.1f} us; last chunk duration p50 {np.nanmedian(dur):.1f} p90 "
-          f"{np.nanpercentile(dur, 90):.1f} max {np.nanmax(dur):.1f} us", flush=True)
+    longest = r3[:, 0] / 100.0
+    over100 = r3[:, 1]
+    qout = np.where(r3[:, 2] > 0, (r3[:, 2] - t0) / 100.0, np.nan)
+    span, first_out = ext.max(), ext.min()
+    q0 = np.nanmin(qout)
+    print(f"    tail {span - first_out:.1f} us (first wave out {first_out:.1f}); global queue first seen out at "
+          f"{q0:.1f}, by the last wave at {np.nanmax(qout):.1f}", flush=True)
+    print(f"    longest chunk per wave p50 {np.median(longest):.1f} p90 {np.percentile(longest, 90):.1f} max "
+          f"{longest.max():.1f} us; chunks over 100 us: {int(over100.sum())} in {int((over100 > 0).sum())} waves "
+          f"(of {int(raw[wid, 3].sum())} chunks)", flush=True)
+    print(f"    last chunk: {int(is_tail.sum())} waves ended on a tail chunk; duration p50 {np.nanmedian(dur):.1f} "
+          f"p90 {np.nanpercentile(dur, 90):.1f} max {np.nanmax(dur):.1f} us", flush=True)
     for x in sorted(set(xcc.tolist())):
         m = xcc == x
         e = ext[m]
         print(f"    XCD {x}: {m.sum():5d} waves, exit min/p50/p90/max {e.min():7.1f}/{np.median(e):7.1f}/"
-              f"{np.percentile(e, 90):7.1f}/{e.max():7.1f}, last chunk p50/max {np.nanmedian(dur[m]):6.1f}/"
-              f"{np.nanmax(dur[m]):6.1f}", flush=True)
-    # the last 2 % of exits: were they waves with a long last chunk, or late starters?
+              f"{np.percentile(e, 90):7.1f}/{e.max():7.1f}", flush=True)
     k = max(1, len(ext) // 50)
     idx = np.argsort(ext)[-k:]
     lstart = np.where(ok, (last - t0) / 100.0, np.nan)
-    print(f"    last {k} waves out: exit {ext[idx].min():.1f}..{ext[idx].max():.1f}, last chunk started "
-          f"p50 {np.nanmedian(lstart[idx]):.1f} (queue empty ~{first_out:.1f}), lasted p50 {np.nanmedian(dur[idx]):.1f} "
-          f"max {np.nanmax(dur[idx]):.1f} us; XCDs {np.bincount(xcc[idx].astype(int), minlength=8).tolist()}",
-          flush=True)
+    print(f"    last {k} waves out (exit {ext[idx].min():.1f}..{ext[idx].max():.1f}): last chunk started p10/p50/p90 "
+          f"{np.nanpercentile(lstart[idx], 10):.1f}/{np.nanmedian(lstart[idx]):.1f}/{np.nanpercentile(lstart[idx], 90):.1f}"
+          f", {int(is_tail[idx].sum())} were tail chunks, lasted p50 {np.nanmedian(dur[idx]):.1f} max "
+          f"{np.nanmax(dur[idx]):.1f} us; saw the queue out at p50 {np.nanmedian(qout[idx]):.1f}; "
+          f"XCDs {np.bincount(xcc[idx].astype(int), minlength=8).tolist()}", flush=True)
+    # waves still running a chunk that started before the queue ran out: how long did those chunks take?
+    pre = ok & (lstart < q0)
+    if pre.any():
+        print(f"    last chunks started before the queue ran out ({int(pre.sum())} waves): lasted p50 "
+              f"{np.nanmedian(dur[pre]):.1f} p90 {np.nanpercentile(dur[pre], 90):.1f} max {np.nanmax(dur[pre]):.1f} us",
+              flush=True)
 
 
 def main():
@@ -74,7 +91,7 @@ def main():
         r.set_option(int(k), int(v))
     r.upload_scene(Scene.build(maze_n, 0))
     u = default_uniform(W, H, 0)
-    ts = torch.zeros((65536, 4), dtype=torch.int64, device="cuda")
+    ts = torch.zeros((3 * TIMELINE_WAVES, 4), dtype=torch.int64, device="cuda")
     print(f"# {desc}; times in us (wall_clock64, 100 MHz)")
     for n in [int(x) for x in a.ranks.split(",")]:
         y0, stride, rows = row_shard(H, n, 0)
@@ -93,7 +110,7 @@ def main():
             launch(f)
             torch.cuda.synchronize()
             r.set_wave_timeline(None)
-            t = ts.cpu().numpy()
+            t = ts.cpu().numpy()[:TIMELINE_WAVES]
             t = t[t[:, 2] > 0]
             t0 = t[:, 0].min()
             ent, stg, ext, ch = ((t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0, t[:, 3])
@@ -107,7 +124,7 @@ def main():
                   flush=True)
             # what balancing the last chunks' paths inside each block could reach: a block's waves
             # finish together at their mean exit (blocks = consecutive 16-wave groups by wave id)
-            wid = np.nonzero(ts.cpu().numpy()[:, 2] > 0)[0]
+            wid = np.nonzero(ts.cpu().numpy()[:TIMELINE_WAVES, 2] > 0)[0]
             blk = wid // 16
             bmean = np.array([ext[blk == b].mean() for b in np.unique(blk)])
             print(f"    block-balanced bound: last block mean exit {bmean.max():7.1f} (vs last wave {span:7.1f}); "
