@@ -212,8 +212,15 @@ def pmc_profile(args, frames_per_launch, k_avg_s, world):
     rec = json.loads(f.read_text())
     here = src_hash()
     if rec.get("src_hash") != here:
-        return {"source": str(f.relative_to(REPO)), "stale": True, "profile_src_hash": rec.get("src_hash"),
-                "src_hash": here, "note": "profile of other kernel sources: not used"}, None
+        # other kernel sources: only its executed lane-ops per frame, scaled to this run's frames per launch, is
+        # offered (labelled) as the headline's basis -- closer to what the kernel executes than the
+        # reference-walk model; its HBM bytes are not used
+        stale = {"source": str(f.relative_to(REPO)), "stale": True, "profile_src_hash": rec.get("src_hash"),
+                 "src_hash": here, "note": "profile of other kernel sources: HBM bytes not used"}
+        if rec.get("valu_lane_ops_per_launch") and rec.get("frames_per_launch"):
+            per_frame = rec["valu_lane_ops_per_launch"] / rec["frames_per_launch"]
+            stale["stale_valu_lane_ops_tops"] = round(per_frame * frames_per_launch / k_avg_s / 1e12, 3)
+        return stale, None
     scale = frames_per_launch / rec["frames_per_launch"]
     hbm = rec["hbm_bytes_per_launch"] * scale
     m = {"source": str(f.relative_to(REPO)), "src_hash": here, "git_head": rec.get("git_head"),
@@ -238,20 +245,25 @@ def roofline(ops, alg_bytes, k_avg_s, k_launches, frames_per_launch, measured, t
     hardware's executed fp32 VALU lane-ops per launch from the same-source PMC
     record (SQ_INSTS_VALU x 64 x lane utilisation) / this run's mean launch
     time, against 78.6 T lane-ops/s.  Without a PMC
-    record of these sources the headline falls back to the reference-walk
-    model and says so in "basis".  The reference-walk VALU model and the
+    record of these sources the headline falls back to a record of other
+    sources (its lane-ops per frame, labelled STALE in "basis"), else to the
+    reference-walk model, and says so in "basis".  The reference-walk VALU model and the
     136 B/ray HBM model are kept as labelled sub-objects."""
     ref_tops = ops / k_avg_s / 1e12
     lane_tops = measured.get("valu_lane_ops_tops") if isinstance(measured, dict) else None
+    stale_tops = measured.get("stale_valu_lane_ops_tops") if isinstance(measured, dict) else None
     hw = lane_tops is not None
-    achieved = lane_tops if hw else ref_tops
+    achieved = lane_tops if hw else (stale_tops if stale_tops is not None else ref_tops)
     return {
         "bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS, "unit": "TFLOP/s",
         "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
         "basis": ("executed fp32 VALU lane-ops (PMC: SQ_INSTS_VALU x 64 x SQ_THREAD_CYCLES_VALU / "
                   "(64 SQ_ACTIVE_INST_VALU), profiles/pmc_<config>.json of these sources) per launch / mean "
                   "launch time" if hw else
-                  "reference_equivalent: no PMC record of these sources (see reference_equivalent)"),
+                  ("STALE: executed fp32 VALU lane-ops per frame of the PMC record of other kernel sources "
+                   "(measured.profile_src_hash), x this run's frames per launch / mean launch time -- not "
+                   "measured on these sources" if stale_tops is not None else
+                   "reference_equivalent: no PMC record of these sources (see reference_equivalent)")),
         "peak_basis": "256 CU x 4 SIMD x 32 fp32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md)",
         "kernel": "k_trace_wavepersist", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
         "launches": k_launches, "frames_per_launch": round(frames_per_launch, 3),
