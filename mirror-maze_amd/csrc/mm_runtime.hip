@@ -79,6 +79,7 @@ struct mm_ctx {
     uint32_t tail_cap = 0;
     // aux: stats[4] (u64) + error flag (u32)
     unsigned long long* d_aux = nullptr;
+    uint32_t* d_work = nullptr;  // the wave-persistent kernel's self-cleaning queue heads + waves-done word (4 KB)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.0f;
     uint32_t last_launches = 0;
@@ -406,6 +407,8 @@ int mm_create(int device, mm_ctx** out) {
     if (rc == MM_OK) chk(hipEventCreate(&c->ev1), "hipEventCreate");
     if (rc == MM_OK) chk(hipMalloc((void**)&c->d_aux, 8 * sizeof(unsigned long long)), "hipMalloc(aux)");
     if (rc == MM_OK) chk(hipMemset(c->d_aux, 0, 8 * sizeof(unsigned long long)), "hipMemset(aux)");
+    if (rc == MM_OK) chk(hipMalloc((void**)&c->d_work, 4096), "hipMalloc(work)");
+    if (rc == MM_OK) chk(hipMemset(c->d_work, 0, 4096), "hipMemset(work)");
     if (rc == MM_OK)
         chk(hipHostMalloc((void**)&c->h_status, (kStatusSlots + kRingDiagWords) * sizeof(uint32_t),
                           hipHostMallocMapped | hipHostMallocCoherent),
@@ -432,7 +435,7 @@ void mm_destroy(mm_ctx* c) {
     free_scene(c);
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
-    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_tail);
+    (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_tail); (void)hipFree(c->d_work);
     if (c->h_status) (void)hipHostFree(c->h_status);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1023,7 +1026,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     TailQueue tq;
     if (defer && ring == 1 && (rc = tail_queue(c, tq))) return rc;  // (records in LDS: no global ring)
     // aux: [0..3] stats (zeroed only when counted), [4] error flag (moved into the launch's status word by
-    // the launch itself), [5] lane-refill counter (zeroed by its launcher), [6] wave-persistent counter pair
+    // the launch itself).  d_work: the wave-persistent kernel's queue head(s) and waves-done word
     // (self-cleaning).  No fill kernel on the default path: see k_trace_wavepersist.
     if (want_stats) HIPC(c, hipMemsetAsync(c->d_aux, 0, 4 * sizeof(unsigned long long), c->stream));
     if ((rc = begin_timing(c))) return rc;
@@ -1073,7 +1076,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                 c->last_kern_form = form;
                 c->last_kern_ring = defer ? ring : 0;
                 HIPC(c, launch_trace_wavepersist(sc, job, c->d_samples, c->d_aux, err_dev,
-                                                 reinterpret_cast<uint32_t*>(c->d_aux + 6), want_stats, mode, form,
+                                                 c->d_work, want_stats, mode, form,
                                                  c->stream));
             } else {
                 MegaOpts mo;

@@ -362,6 +362,10 @@ __device__ __forceinline__ void poison(float4* samples, uint32_t slot, uint32_t 
 #define MM_CLAIM_CHUNKS 4
 #endif
 constexpr uint32_t kClaimChunks = MM_CLAIM_CHUNKS;  // chunks per dequeue (A/B: -DMM_CLAIM_CHUNKS=k)
+#ifndef MM_CLAIM_TAIL
+#define MM_CLAIM_TAIL 1
+#endif
+constexpr uint32_t kClaimTail = MM_CLAIM_TAIL;  // single claims for the last kClaimTail x (waves x big) paths
 
 // The next 64-path chunk of the global queue for this wave (its first path;
 // >= n_queue: the queue is out).  Claims of kClaimChunks chunks per returning
@@ -372,14 +376,15 @@ constexpr uint32_t kClaimChunks = MM_CLAIM_CHUNKS;  // chunks per dequeue (A/B: 
 // The wave's claimed range [next, end) lives in LDS, not in registers held
 // across the bounce loop (SGPR pressure there spills into VGPR lanes).
 #ifdef MM_TAIL_CLOCKS
-constexpr uint32_t kClaimWords = 8;
+constexpr uint32_t kClaimWords = 10;
 #else
-constexpr uint32_t kClaimWords = 2;
+constexpr uint32_t kClaimWords = 3;
 #endif
 __device__ __forceinline__ uint32_t* claim_words() {
-    // (next, end) per wave of a <= 1024-thread block; diagnostics build MM_TAIL_CLOCKS: then the wall clock at
-    // the start of the wave's current chunk (lo, hi), its longest chunk so far (10 ns units), its chunks over
-    // 100 us, the clock when it saw the global queue out (lo, hi)
+    // (next, end, head) per wave of a <= 1024-thread block (head: MM_XCD_HEADS, the queue head the wave
+    // pulls from); diagnostics build MM_TAIL_CLOCKS: then the wall clock at the start of the wave's current
+    // chunk (lo, hi), its longest chunk so far (10 ns units), its chunks over 100 us, the clock when it saw
+    // the global queue out (lo, hi)
     __shared__ uint32_t w[kClaimWords * 16];
     return w + kClaimWords * (threadIdx.x >> 6);
 }
@@ -392,14 +397,14 @@ __device__ __forceinline__ void mark_chunk_start(const TileJob& job, uint32_t ki
     if (job.wave_ts && (threadIdx.x & 63u) == 0) {
         uint32_t* cw = claim_words();
         const uint64_t t = wall_clock64();
-        const uint64_t prev = cw[2] | (uint64_t)cw[3] << 32;
+        const uint64_t prev = cw[4] | (uint64_t)(cw[5] & 0x7FFFFFFFu) << 32;
         if (prev) {
             const uint32_t d = (uint32_t)min<uint64_t>(t - prev, 0xFFFFFFFFull);
-            cw[4] = max(cw[4], d);
-            cw[5] += d > 10000u ? 1u : 0u;
+            cw[6] = max(cw[6], d);
+            cw[7] += d > 10000u ? 1u : 0u;
         }
-        cw[2] = (uint32_t)t;
-        cw[3] = (uint32_t)(t >> 32) | (kind << 31);
+        cw[4] = (uint32_t)t;
+        cw[5] = (uint32_t)(t >> 32) | (kind << 31);
     }
 #endif
 }
@@ -407,23 +412,29 @@ __device__ __forceinline__ void mark_queue_out(const TileJob& job) {
 #ifndef MM_TAIL_CLOCKS
     (void)job;
 #else
-    if (job.wave_ts && (threadIdx.x & 63u) == 0 && !claim_words()[7]) {
+    if (job.wave_ts && (threadIdx.x & 63u) == 0 && !claim_words()[9]) {
         const uint64_t t = wall_clock64();
-        claim_words()[6] = (uint32_t)t;
-        claim_words()[7] = (uint32_t)(t >> 32);
+        claim_words()[8] = (uint32_t)t;
+        claim_words()[9] = (uint32_t)(t >> 32);
     }
 #endif
 }
 __device__ __forceinline__ void claim_reset() {
-    if ((threadIdx.x & 63u) == 0)
+    if ((threadIdx.x & 63u) == 0) {
         for (uint32_t i = 0; i < kClaimWords; ++i) claim_words()[i] = 0u;
+#ifdef MM_XCD_HEADS
+        claim_words()[2] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // hwreg(HW_REG_XCC_ID, 0, 4): 0-7
+#endif
+    }
 }
+#ifndef MM_XCD_HEADS
+constexpr uint32_t kDoneWord = 1;  // work[0] = next path, work[1] = waves done
 __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
     uint32_t* cw = claim_words();
     uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
     if (next >= end) {
         const uint32_t big = kClaimChunks * 64u;
-        const uint32_t tail = gridDim.x * (blockDim.x >> 6) * big;  // paths left below which claims are single
+        const uint32_t tail = kClaimTail * gridDim.x * (blockDim.x >> 6) * big;  // below: single claims
         const uint32_t k = (n_queue > tail && next < n_queue - tail) ? big : 64u;
         uint32_t b = 0;
         if ((threadIdx.x & 63u) == 0) b = atomicAdd(work, k);
@@ -433,6 +444,44 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
     if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
     return next;
 }
+#else
+// Per-XCD queue heads (MM_XCD_HEADS; MI355X_MICROARCH.md "dequeue": one head word saturates at ~88
+// dequeues/us, shard it above 64 pullers): the queue's chunks are dealt to 8 heads in contiguous eighths,
+// head h at work[h * kHeadStride]; a wave pulls from its XCD's head (HW_REG_XCC_ID) and, once that is out,
+// from the next ones in turn; the queue is out when all 8 are.  kClaimChunks chunks per claim down to the
+// head's last kClaimTail x (its waves x claim) paths, then single chunks.
+constexpr uint32_t kHeadStride = 32;              // 128 B apart
+constexpr uint32_t kDoneWord = 8 * kHeadStride;  // waves done
+__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
+    uint32_t* cw = claim_words();
+    uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
+    if (next >= end) {
+        const uint32_t per = ((n_queue / 64u + 7u) / 8u) * 64u;  // paths per head
+        const uint32_t big = kClaimChunks * 64u;
+        const uint32_t tail = kClaimTail * (gridDim.x * (blockDim.x >> 6) / 8u) * big;
+        uint32_t h = __builtin_amdgcn_readfirstlane(cw[2]);
+        next = end = n_queue;
+        for (uint32_t tries = 0; tries < 8u; ++tries, h = (h + 1u) & 7u) {
+            const uint32_t lo = min(h * per, n_queue), hi = min(lo + per, n_queue);
+            if (lo >= hi) continue;
+            const uint32_t last = __builtin_amdgcn_readfirstlane(cw[0]);
+            const uint32_t done = last >= lo && last <= hi ? last - lo : 0u;  // where this wave last claimed here
+            const uint32_t k = (per > tail && done < per - tail) ? big : 64u;
+            uint32_t b = 0;
+            if ((threadIdx.x & 63u) == 0) b = atomicAdd(work + h * kHeadStride, k);
+            b = __builtin_amdgcn_readfirstlane(b);
+            if (b < hi - lo) {
+                next = lo + b;
+                end = min(next + k, hi);
+                break;
+            }
+        }
+        if ((threadIdx.x & 63u) == 0) cw[2] = h;
+    }
+    if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
+    return next;
+}
+#endif
 
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
@@ -785,14 +834,14 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
             const uint32_t* cw = claim_words();
             const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);   // hwreg(HW_REG_XCC_ID, 0, 4)
             const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // hwreg(HW_REG_HW_ID, 0, 32)
-            job.wave_ts[4 * wid + 0] = cw[2] | (unsigned long long)cw[3] << 32;
+            job.wave_ts[4 * wid + 0] = cw[4] | (unsigned long long)cw[5] << 32;
             job.wave_ts[4 * wid + 1] = xcc;
             job.wave_ts[4 * wid + 2] = hwid;
             job.wave_ts[4 * wid + 3] = chunks;
             const uint32_t w2 = wid + kTimelineWaves;
-            job.wave_ts[4 * w2 + 0] = cw[4];
-            job.wave_ts[4 * w2 + 1] = cw[5];
-            job.wave_ts[4 * w2 + 2] = cw[6] | (unsigned long long)cw[7] << 32;
+            job.wave_ts[4 * w2 + 0] = cw[6];
+            job.wave_ts[4 * w2 + 1] = cw[7];
+            job.wave_ts[4 * w2 + 2] = cw[8] | (unsigned long long)cw[9] << 32;
             job.wave_ts[4 * w2 + 3] = (unsigned long long)wall_clock64();
         }
     }
@@ -800,9 +849,13 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
     if ((threadIdx.x & 63u) == 0) {
         __threadfence();
         const uint32_t total = gridDim.x * (blockDim.x >> 6);
-        if (atomicAdd(counter + 1, 1u) == total - 1) {
+        if (atomicAdd(counter + kDoneWord, 1u) == total - 1) {
+#ifdef MM_XCD_HEADS
+            for (uint32_t h = 0; h < 8u; ++h) atomicExch(counter + h * kHeadStride, 0u);
+#else
             atomicExch(counter, 0u);
-            atomicExch(counter + 1, 0u);
+#endif
+            atomicExch(counter + kDoneWord, 0u);
             if (job.status) {
                 const uint32_t e = atomicExch(err, 0u);
                 __hip_atomic_store(job.status, e | kStatusDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1,5 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out/r4c
-MIRROR_MAZE_LIB=exp/tailclk/lib.so timeout -k 10 300 python -u scripts/timeline_probe.py --config c3 --ranks 1,8 --batch 20 --frames 2 --tail > gpurun_out/r4c/tail_probe.txt 2>&1 || exit $?
-grep -v amdgpu.ids gpurun_out/r4c/tail_probe.txt
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/r4c/tests.log 2>&1; rc=$?; tail -3 gpurun_out/r4c/tests.log; exit $rc
+for L in tailclk tc_claim1 tc_tail4 tc_heads tc_heads1; do
+  echo "## $L"
+  MIRROR_MAZE_LIB=exp/$L/lib.so timeout -k 10 300 python -u scripts/timeline_probe.py --config c3 --ranks 1,8 --batch 20 --frames 2 --tail > gpurun_out/r4c/tail_probe_$L.txt 2>&1 || exit $?
+  grep -v amdgpu.ids gpurun_out/r4c/tail_probe_$L.txt | grep -v "XCD [1-7]" | grep -v "block-balanced"
+done
+timeout -k 10 900 python -u scripts/ab.py --tag r4c --config c3:20:3 --config c4:2:2 --lib exp/base/lib.so --lib exp/heads/lib.so --lib exp/heads1/lib.so 2>&1 | tail -8
+timeout -k 10 600 python -u scripts/ab.py --tag r4c8 --ranks 8 --config c3:20:3 --lib exp/base/lib.so --lib exp/heads/lib.so --lib exp/heads1/lib.so 2>&1 | tail -5
