@@ -427,9 +427,26 @@ __device__ __forceinline__ void claim_reset() {
 #endif
     }
 }
+// Progress-fair wave priority (MM_FAIR_PRIO, A/B): the SIMD's arbiter favours older waves, and in a
+// persistent launch the oldest waves of a SIMD take several times the chunks of the youngest (C3: 184 to
+// 1,523 chunks per wave, profiles/r04/tail_probe_*.txt); at the queue's end the young waves are then still
+// several of their (long) chunks from done.  Each claim sets the wave's priority from how far it is
+// behind the chip's mean chunks per wave (head / 64 / waves), so the waves finish together.
+__device__ __forceinline__ void fair_prio(uint32_t head, uint32_t chunks_done) {
+#ifdef MM_FAIR_PRIO
+    const uint32_t mean = head / (64u * gridDim.x * (blockDim.x >> 6));
+    if (chunks_done + 8u < mean) __builtin_amdgcn_s_setprio(3);
+    else if (chunks_done + 4u < mean) __builtin_amdgcn_s_setprio(2);
+    else if (chunks_done < mean) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)head; (void)chunks_done;
+#endif
+}
+
 #ifndef MM_XCD_HEADS
 constexpr uint32_t kDoneWord = 1;  // work[0] = next path, work[1] = waves done
-__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
+__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue, uint32_t chunks_done) {
     uint32_t* cw = claim_words();
     uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
     if (next >= end) {
@@ -440,6 +457,7 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
         if ((threadIdx.x & 63u) == 0) b = atomicAdd(work, k);
         next = __builtin_amdgcn_readfirstlane(b);
         end = min(next + k, n_queue);
+        fair_prio(next, chunks_done);
     }
     if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
     return next;
@@ -452,7 +470,8 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
 // head's last kClaimTail x (its waves x claim) paths, then single chunks.
 constexpr uint32_t kHeadStride = 32;              // 128 B apart
 constexpr uint32_t kDoneWord = 8 * kHeadStride;  // waves done
-__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
+__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue, uint32_t chunks_done) {
+    (void)chunks_done;
     uint32_t* cw = claim_words();
     uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
     if (next >= end) {
@@ -498,7 +517,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     uint32_t paths = 0, chunks = 0;
     claim_reset();
     for (;;) {
-        const uint32_t base = dequeue(work, n_queue);
+        const uint32_t base = dequeue(work, n_queue, chunks);
         if (base >= n_queue) {
             mark_queue_out(job);
             break;
@@ -604,7 +623,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
 #endif
                 continue;
             }
-            b = dequeue(work, n_queue);
+            b = dequeue(work, n_queue, chunks);
             if (b >= n_queue) {
                 defer_from = 1 << 30;
                 mark_queue_out(job);
