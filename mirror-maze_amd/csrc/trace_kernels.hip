@@ -453,6 +453,14 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue, ui
         const uint32_t big = kClaimChunks * 64u;
         const uint32_t tail = kClaimTail * gridDim.x * (blockDim.x >> 6) * big;  // below: single claims
         const uint32_t k = (n_queue > tail && next < n_queue - tail) ? big : 64u;
+#ifdef MM_TAIL_RETIRE
+        // (A/B) in the single-claim zone a wave that has done under half the chip's mean chunks takes no
+        // more: its next chunk would be among the last to finish
+        if (k == 64u && next > 0u && chunks_done < next / (128u * gridDim.x * (blockDim.x >> 6))) {
+            if ((threadIdx.x & 63u) == 0) { cw[0] = n_queue + 64u; cw[1] = n_queue; }
+            return n_queue;
+        }
+#endif
         uint32_t b = 0;
         if ((threadIdx.x & 63u) == 0) b = atomicAdd(work, k);
         next = __builtin_amdgcn_readfirstlane(b);
