@@ -376,7 +376,7 @@ constexpr uint32_t kClaimTail = MM_CLAIM_TAIL;  // single claims for the last kC
 // The wave's claimed range [next, end) lives in LDS, not in registers held
 // across the bounce loop (SGPR pressure there spills into VGPR lanes).
 #ifdef MM_TAIL_CLOCKS
-constexpr uint32_t kClaimWords = 10;
+constexpr uint32_t kClaimWords = 16;
 #else
 constexpr uint32_t kClaimWords = 3;
 #endif
@@ -400,8 +400,12 @@ __device__ __forceinline__ void mark_chunk_start(const TileJob& job, uint32_t ki
         const uint64_t prev = cw[4] | (uint64_t)(cw[5] & 0x7FFFFFFFu) << 32;
         if (prev) {
             const uint32_t d = (uint32_t)min<uint64_t>(t - prev, 0xFFFFFFFFull);
+            const uint32_t pk = cw[5] >> 31;  // the previous chunk's kind
             cw[6] = max(cw[6], d);
             cw[7] += d > 10000u ? 1u : 0u;
+            cw[10 + 2 * pk] += d;  // per kind (new / tail): summed duration, count, longest
+            cw[11 + 2 * pk] += 1u;
+            cw[14 + pk] = max(cw[14 + pk], d);
         }
         cw[4] = (uint32_t)t;
         cw[5] = (uint32_t)(t >> 32) | (kind << 31);
@@ -870,6 +874,13 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
             job.wave_ts[4 * w2 + 1] = cw[7];
             job.wave_ts[4 * w2 + 2] = cw[8] | (unsigned long long)cw[9] << 32;
             job.wave_ts[4 * w2 + 3] = (unsigned long long)wall_clock64();
+            const uint32_t w3 = w2 + kTimelineWaves;  // per chunk kind: (sum << 32 | count), longest
+            if (w3 < job.wave_ts_cap) {
+                job.wave_ts[4 * w3 + 0] = (unsigned long long)cw[10] << 32 | cw[11];
+                job.wave_ts[4 * w3 + 1] = (unsigned long long)cw[12] << 32 | cw[13];
+                job.wave_ts[4 * w3 + 2] = cw[14];
+                job.wave_ts[4 * w3 + 3] = cw[15];
+            }
         }
     }
 #endif

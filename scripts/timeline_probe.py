@@ -58,6 +58,15 @@ def tail_report(raw, t0, np):
           f", {int(is_tail[idx].sum())} were tail chunks, lasted p50 {np.nanmedian(dur[idx]):.1f} max "
           f"{np.nanmax(dur[idx]):.1f} us; saw the queue out at p50 {np.nanmedian(qout[idx]):.1f}; "
           f"XCDs {np.bincount(xcc[idx].astype(int), minlength=8).tolist()}", flush=True)
+    r4 = raw[3 * n + wid].astype(np.uint64)
+    if r4[:, 0].any():
+        for kind, col in (("new", 0), ("tail", 1)):
+            tot = (r4[:, col] >> np.uint64(32)).astype(np.float64) / 100.0
+            cnt = (r4[:, col] & np.uint64(0xFFFFFFFF)).astype(np.float64)
+            lng = r4[:, 2 + col].astype(np.float64) / 100.0
+            print(f"    {kind} chunks: {int(cnt.sum())}, mean {tot.sum() / max(cnt.sum(), 1):.1f} us, longest per wave "
+                  f"p50 {np.median(lng):.1f} p90 {np.percentile(lng, 90):.1f} max {lng.max():.1f} us; share of wave "
+                  f"time {tot.sum() / (ext.sum() + 1e-9):.1%}", flush=True)
     # waves still running a chunk that started before the queue ran out: how long did those chunks take?
     pre = ok & (lstart < q0)
     if pre.any():
@@ -91,7 +100,7 @@ def main():
         r.set_option(int(k), int(v))
     r.upload_scene(Scene.build(maze_n, 0))
     u = default_uniform(W, H, 0)
-    ts = torch.zeros((3 * TIMELINE_WAVES, 4), dtype=torch.int64, device="cuda")
+    ts = torch.zeros((4 * TIMELINE_WAVES, 4), dtype=torch.int64, device="cuda")
     print(f"# {desc}; times in us (wall_clock64, 100 MHz)")
     for n in [int(x) for x in a.ranks.split(",")]:
         y0, stride, rows = row_shard(H, n, 0)
