@@ -447,6 +447,26 @@ __device__ __forceinline__ void fair_prio(uint32_t head, uint32_t chunks_done) {
     (void)head; (void)chunks_done;
 #endif
 }
+// End-of-queue priority (MM_END_PRIO=z, A/B): the last waves out are their SIMD's youngest (launch
+// order 7 of 8 in 123 of the last 163; profiles/r04/tail_probe/tail_probe_simd.txt), whose chunks run
+// at a seventh of the oldest's rate until the old waves exit.  From the last z x (waves x claim) paths
+// of the queue on, each chunk start sets the wave's priority from its deficit against the chip's mean
+// chunks per wave, so a SIMD's waves finish their last chunks together.
+__device__ __forceinline__ void end_prio(uint32_t next, uint32_t n_queue, uint32_t chunks_done) {
+#ifdef MM_END_PRIO
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t zone = MM_END_PRIO * waves * kClaimChunks * 64u;
+    if (next < n_queue && (n_queue <= zone || next >= n_queue - zone)) {
+        const uint32_t mean = next / (64u * waves);
+        if (2u * chunks_done < mean) __builtin_amdgcn_s_setprio(3);
+        else if (4u * chunks_done < 3u * mean) __builtin_amdgcn_s_setprio(2);
+        else if (chunks_done < mean) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+#else
+    (void)next; (void)n_queue; (void)chunks_done;
+#endif
+}
 
 #ifndef MM_XCD_HEADS
 constexpr uint32_t kDoneWord = 1;  // work[0] = next path, work[1] = waves done
@@ -471,6 +491,7 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue, ui
         end = min(next + k, n_queue);
         fair_prio(next, chunks_done);
     }
+    end_prio(next, n_queue, chunks_done);
     if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
     return next;
 }

@@ -67,6 +67,34 @@ def tail_report(raw, t0, np):
             print(f"    {kind} chunks: {int(cnt.sum())}, mean {tot.sum() / max(cnt.sum(), 1):.1f} us, longest per wave "
                   f"p50 {np.median(lng):.1f} p90 {np.percentile(lng, 90):.1f} max {lng.max():.1f} us; share of wave "
                   f"time {tot.sum() / (ext.sum() + 1e-9):.1%}", flush=True)
+    # per SIMD (HW_REG_HW_ID: simd [5:4], cu [11:8], sh [12], se [15:13], with the XCD): the waves sharing
+    # it, ordered by launch (wave id), their chunks and exits -- does the issue arbiter's age order set a
+    # wave's speed, and are the last waves out the young ones?
+    hw = r2[:, 2].astype(np.int64)
+    simd = ((xcc.astype(np.int64) << 16) | (((hw >> 13) & 7) << 12) | (((hw >> 12) & 1) << 11) |
+            (((hw >> 8) & 15) << 4) | ((hw >> 4) & 3))
+    chunks = raw[wid, 3].astype(np.float64)
+    order = np.lexsort((wid, simd))
+    s_sorted = simd[order]
+    starts = np.r_[0, np.nonzero(np.diff(s_sorted))[0] + 1]
+    age = np.empty(len(wid), dtype=np.int64)  # 0: the SIMD's first-launched wave
+    for a, b in zip(starts, np.r_[starts[1:], len(order)]):
+        age[order[a:b]] = np.arange(b - a)
+    per = np.bincount(simd_idx := np.unique(simd, return_inverse=True)[1])
+    print(f"    SIMDs {len(per)}, waves per SIMD {np.bincount(per).nonzero()[0].tolist()}", flush=True)
+    rows = []
+    for g in range(int(age.max()) + 1):
+        m = age == g
+        rows.append(f"{g}:{chunks[m].mean():.0f}/{np.median(ext[m]) - first_out:.0f}")
+    print("    by launch order on the SIMD (order: mean chunks / median exit after the first wave out, us): "
+          + " ".join(rows), flush=True)
+    rk = np.empty(len(wid), dtype=np.int64)  # 0: the SIMD's busiest wave
+    for a, b in zip(starts, np.r_[starts[1:], len(order)]):
+        o = order[a:b]
+        rk[o[np.argsort(-chunks[o], kind="stable")]] = np.arange(b - a)
+    print(f"    last {k} waves out: launch order on their SIMD {np.bincount(age[idx], minlength=age.max() + 1).tolist()}"
+          f", chunk rank on their SIMD (0 = most) {np.bincount(rk[idx], minlength=rk.max() + 1).tolist()}; their "
+          f"chunks p50 {np.median(chunks[idx]):.0f} (all waves p50 {np.median(chunks):.0f})", flush=True)
     # waves still running a chunk that started before the queue ran out: how long did those chunks take?
     pre = ok & (lstart < q0)
     if pre.any():
