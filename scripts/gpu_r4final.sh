@@ -1,10 +1,10 @@
-# Round-4 final GPU record of HEAD (after scripts/gpu_r4pmc.sh's records are committed): the -m gpu suite,
-# smoke, the default bench line (the driver's command), every configuration's bench line
+# Round-4 final GPU record of HEAD (after the PMC records are committed; the -m gpu suite ran on the same
+# sources in scripts/gpu_r4p1.sh): smoke, the default bench line (the driver's command), every configuration's bench line
 # (scripts/gpu_results.sh), C5 as BASELINE states it (120 accumulated frames) and the rocprofv3 --stats
 # summaries of the C2 / C4 / C5-120 bench commands.
 set -o pipefail
 T=${1:-r4f}
-bash scripts/gpu_steps.sh $T "900|tests|python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+bash scripts/gpu_steps.sh $T \
   "120|smoke|python -c 'import __graft_entry__ as g; g.smoke()'" \
   "200|bench|python bench.py --steps 20 --warmup 5" || exit $?
 bash scripts/gpu_results.sh ${T}res || exit $?

@@ -17,17 +17,20 @@ for f in sys.argv[1:]:
 order = {"C1": 1, "C2": 2, "C3": 3, "C4": 4, "C5": 5}
 rows.sort(key=lambda d: (order.get(d["config"]["workload"][:2], 9), d["config"]["workload"],
                          d["config"]["parallelism"]))
-print("| config | GPU (1 x MI355X) | ms/frame | CPU 1 core | CPU (usable cores) | executed VALU lane-ops (PMC) |"
+print("| config | GPU (1 x MI355X) | ms/frame | CPU 1 core | CPU (usable cores), reference walk | CPU (usable cores), "
+      "same algorithm | executed VALU lane-ops (PMC) |"
       " VALU roofline (ref.-walk model) | HBM model (136 B/ray) |")
-print("|---|---|---|---|---|---|---|---|")
+print("|---|---|---|---|---|---|---|---|---|")
 for d in rows:
     c, r, cb = d["config"], d["roofline"], d.get("cpu_baseline") or {}
     sc = cb.get("single_core") or {}
-    acc = " (accumulated)" if c.get("temporal_accumulation") else ""
+    acc = f" (accumulated, {d['steps']} frames)" if c.get("temporal_accumulation") else ""
     par = "" if c["parallelism"] == "1 GPU" else f" [{c['parallelism']}]"
     cpu = f"{cb['value']} Mrays/s ({cb['cores']} cores)" if cb else "—"
+    sa = cb.get("same_algorithm") or {}
+    same = f"{sa['value']} Mrays/s ({sa['cores']} cores)" if sa else "—"
     ref = r.get("reference_equivalent", r)  # (round-2 lines: the headline was the model)
     hw = (f"{100 * r['frac']:.1f} % of {r['peak']} T" if r.get("basis", "").startswith("executed") else "—")
     print(f"| {c['workload']}{acc}{par} | {d['value']:.0f} Mrays/s | {d['ms_per_step']:.3f} | "
-          f"{sc.get('value', '—')} Mrays/s | {cpu} | {hw} | {100 * ref['frac']:.1f} % of {r['peak']} T | "
+          f"{sc.get('value', '—')} Mrays/s | {cpu} | {same} | {hw} | {100 * ref['frac']:.1f} % of {r['peak']} T | "
           f"{100 * r['model_hbm']['frac']:.1f} % |")
