@@ -203,11 +203,14 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
 
 def pmc_profile(args, frames_per_launch, k_avg_s, world):
     """Measured counters of the dominant kernel from profiles/pmc_<config>.json
-    (scripts/pmc_record.py over rocprofv3 --pmc passes of `bench.py --steps 5
-    --warmup 0`), used only when its source hash is this tree's.  Returns
+    (pmc_<config>_r<N>.json for --emulate-ranks N; scripts/pmc_record.py over
+    rocprofv3 --pmc passes of bench.py's own launch), used only when its source
+    hash is this tree's.  Returns
     (measured dict, HBM bytes per launch or None)."""
-    f = REPO / "profiles" / f"pmc_{args.config}.json"
-    if not f.exists() or args.pipeline != "auto" or args.opt or args.emulate_ranks or world > 1:
+    # rank 0's share of an N-way split (--emulate-ranks N) has its own launch shape: pmc_<config>_r<N>.json
+    name = args.config + (f"_r{args.emulate_ranks}" if args.emulate_ranks and args.emulate_ranks > 1 else "")
+    f = REPO / "profiles" / f"pmc_{name}.json"
+    if not f.exists() or args.pipeline != "auto" or args.opt or world > 1:
         return {"source": None, "note": "no PMC profile for this configuration"}, None
     rec = json.loads(f.read_text())
     here = src_hash()
