@@ -95,6 +95,27 @@ def tail_report(raw, t0, np):
     print(f"    last {k} waves out: launch order on their SIMD {np.bincount(age[idx], minlength=age.max() + 1).tolist()}"
           f", chunk rank on their SIMD (0 = most) {np.bincount(rk[idx], minlength=rk.max() + 1).tolist()}; their "
           f"chunks p50 {np.median(chunks[idx]):.0f} (all waves p50 {np.median(chunks):.0f})", flush=True)
+    # each wave's last new chunk (from the global queue): when it started and ended against the queue running out
+    # (q0), and the tail chunks the wave ran after it -- is the drain the last new chunks or the rings' tails?
+    r5 = raw[4 * n + wid].astype(np.uint64)
+    if r5[:, 0].any():
+        ls = (r5[:, 0].astype(np.int64) - t0) / 100.0
+        ld = r5[:, 1].astype(np.float64) / 100.0
+        le = np.where(ld > 0, ls + ld, ext)  # 0: the last new chunk ran until the exit
+        nt = r5[:, 2].astype(np.int64)
+        print(f"    last new chunk ended after the queue ran out: p50 {np.median(le) - q0:.1f} p90 "
+              f"{np.percentile(le, 90) - q0:.1f} max {le.max() - q0:.1f} us; tail chunks after it p50 "
+              f"{np.median(nt):.0f} p90 {np.percentile(nt, 90):.0f} max {nt.max()}", flush=True)
+        print(f"    last {k} waves out: their last new chunk started {np.median(ls[idx]) - q0:.1f} (p50) / "
+              f"{np.min(ls[idx]) - q0:.1f} (min) and ended {np.median(le[idx]) - q0:.1f} (p50) / "
+              f"{np.max(le[idx]) - q0:.1f} (max) us after the queue ran out; tail chunks after it p50 "
+              f"{np.median(nt[idx]):.0f} max {nt[idx].max()}", flush=True)
+        for g in range(int(age.max()) + 1):
+            m = age == g
+            print(f"      launch order {g}: last new chunk ends p50 {np.median(le[m]) - q0:.1f} p90 "
+                  f"{np.percentile(le[m], 90) - q0:.1f} us after q0, lasted p50 "
+                  f"{np.median(np.where(ld[m] > 0, ld[m], ext[m] - ls[m])):.1f} us; tail chunks after p50 "
+                  f"{np.median(nt[m]):.0f}; exit p50 {np.median(ext[m]) - q0:.1f}", flush=True)
     # waves still running a chunk that started before the queue ran out: how long did those chunks take?
     pre = ok & (lstart < q0)
     if pre.any():
@@ -128,7 +149,7 @@ def main():
         r.set_option(int(k), int(v))
     r.upload_scene(Scene.build(maze_n, 0))
     u = default_uniform(W, H, 0)
-    ts = torch.zeros((4 * TIMELINE_WAVES, 4), dtype=torch.int64, device="cuda")
+    ts = torch.zeros((5 * TIMELINE_WAVES, 4), dtype=torch.int64, device="cuda")
     print(f"# {desc}; times in us (wall_clock64, 100 MHz)")
     for n in [int(x) for x in a.ranks.split(",")]:
         y0, stride, rows = row_shard(H, n, 0)
