@@ -31,6 +31,11 @@
 //   re-park at once, without a bounce); bit 1: turn values modulo 2^24 (the
 //   sequence counters are 32-bit: lap = seq / R wraps from 2^32 / R - 1 to 0).
 //   The round-4 kernel is policy 3 (trace_kernels.hip ring_turn_value).
+//   bit 2: the end-of-queue split (MM_END_SPLIT): once a wave has seen the
+//   queue out, a block flag is set; a new chunk from the last 4 x waves chunks
+//   then parks all its live lanes at its next bounce top (>= defer_from), and
+//   every claim made while the flag is set needs 1 entry and takes
+//   avail / (waves / 2) clamped to [lanes / 4, lanes].
 //   seq0 (optional): the counters' start value, the turn words set as if every
 //   earlier entry had been written and read (a ring near the 2^32 wrap).
 //   burst: mean scheduler quantum (1 = every step a fresh random wave).
@@ -73,6 +78,8 @@ struct Wave {
     uint32_t r_cl = 0, r_res = 0, cnt = 0;
     uint64_t wait_start = 0;
     bool tail_chunk = false;
+    bool split = false;  // policy 4: a new chunk from the queue's end zone
+    bool endf = false;   // policy 4: the block flag as this wave's claim read it
     uint32_t busy = 0;  // scheduler steps left in the current bounce
 };
 
@@ -86,11 +93,12 @@ struct Model {
     std::vector<uint32_t> turn;
     std::vector<uint32_t> pay_path, pay_n;
     uint32_t q_next = 0;
+    bool end_flag = false;  // policy 4: a wave has seen the queue out
     std::vector<Wave> w;
     std::vector<uint32_t> T;     // bounces per path
     std::vector<uint32_t> done;  // completions per path
     uint64_t step = 0, last_change = 0, last_progress = 0, bounces = 0;
-    uint64_t max_wait = 0, waits = 0, parks = 0, claims = 0, reserve_fail = 0;
+    uint64_t max_wait = 0, waits = 0, parks = 0, claims = 0, reserve_fail = 0, end_parks = 0;
 
     uint32_t lap(uint32_t seq) const { return seq / R; }
     // turn value (2 lap + c) as the kernel computes it
@@ -112,15 +120,23 @@ struct Model {
     bool exec(uint32_t i) {
         Wave& v = w[i];
         switch (v.pc) {
-            case TOP:  // ring_claim: lane 0 reads claimed ...
+            case TOP:  // ring_claim: lane 0 reads claimed (policy 4: the flag first) ...
+                v.endf = (policy & 4) && end_flag;
                 v.c_cl = claimed;
                 v.pc = CLAIM_RES;
                 return true;
             case CLAIM_RES: {  // ... then reserved
                 v.c_res = reserved;
-                const uint32_t avail = v.c_res - v.c_cl, need = v.off ? 1u : L;
+                const uint32_t avail = v.c_res - v.c_cl, need = (v.off || v.endf) ? 1u : L;
                 if (avail < need) { v.k = 0; v.pc = NOCLAIM; return true; }
-                v.k = avail < L ? avail : L;
+                uint32_t cap = L;
+                if (v.endf) {
+                    const uint32_t lo = L / 4 ? L / 4 : 1, div = W / 2 ? W / 2 : 1;
+                    cap = avail / div;
+                    if (cap < lo) cap = lo;
+                    if (cap > L) cap = L;
+                }
+                v.k = avail < cap ? avail : cap;
                 v.pc = CLAIM_CAS;
                 return true;
             }
@@ -144,9 +160,10 @@ struct Model {
                 v.pc = (reserved - v.left_cl) == 0 ? EXITED : TOP;
                 return true;
             case DEQUEUE:
-                if (q_next >= Q) { v.off = true; v.pc = TOP; return true; }
+                if (q_next >= Q) { v.off = true; end_flag = true; v.pc = TOP; return true; }
                 {
                     const uint32_t c = q_next++;
+                    v.split = (policy & 4) && c + 4 * W >= Q;
                     for (uint32_t j = 0; j < L; ++j) {
                         v.lane[j] = Lane{};
                         v.lane[j].live = true;
@@ -182,6 +199,7 @@ struct Model {
                     turn[slot(s)] = tv(s, 2);
                 }
                 v.tail_chunk = true;
+                v.split = false;
                 v.df = v.off ? kOff : defer_from;
                 if ((policy & 1) && v.k <= defer_lanes) v.df = kOff;  // would re-park at once
                 start_loop(v);
@@ -194,7 +212,7 @@ struct Model {
                     if (l.n >= v.df) ++elig;
                 }
                 if (!in) { v.pc = AFTER; return true; }
-                if (elig && elig <= defer_lanes) {
+                if (elig && (elig <= defer_lanes || (v.split && end_flag))) {
                     v.cnt = elig;
                     v.r_cl = claimed;  // ring_reserve: leader reads claimed ...
                     v.pc = RES_RES;
@@ -215,6 +233,7 @@ struct Model {
                     for (auto& l : v.lane)
                         if (l.in_loop && l.n >= v.df) { l.in_loop = false; l.deferred = true; l.seq = s++; }
                     ++parks;
+                    if (v.split && end_flag) ++end_parks;
                 } else {
                     ++reserve_fail;
                 }
@@ -346,11 +365,11 @@ int main(int argc, char** argv) {
     }
     if (verdict == "ok" && (lost || dup || m.reserved != m.claimed)) verdict = "conservation";
     std::printf("{\"verdict\": \"%s\", \"steps\": %llu, \"bounces\": %llu, \"max_wait\": %llu, \"waits\": %llu, "
-                "\"parks\": %llu, \"claims\": %llu, \"reserve_fail\": %llu, \"lost\": %u, \"dup\": %u, "
+                "\"parks\": %llu, \"end_parks\": %llu, \"claims\": %llu, \"reserve_fail\": %llu, \"lost\": %u, \"dup\": %u, "
                 "\"reserved\": %u, \"claimed\": %u, \"states\": \"",
                 verdict.c_str(), (unsigned long long)m.step, (unsigned long long)m.bounces,
                 (unsigned long long)m.max_wait, (unsigned long long)m.waits, (unsigned long long)m.parks,
-                (unsigned long long)m.claims, (unsigned long long)m.reserve_fail, lost, dup, m.reserved, m.claimed);
+                (unsigned long long)m.end_parks, (unsigned long long)m.claims, (unsigned long long)m.reserve_fail, lost, dup, m.reserved, m.claimed);
     for (uint32_t i = 0; i < m.W; ++i) std::printf("%s%s%s", i ? " " : "", pc_name(m.w[i].pc), m.w[i].off ? "*" : "");
     std::printf("\"}\n");
     return verdict == "ok" ? 0 : 1;

@@ -84,3 +84,29 @@ def test_round4_protocol_small_rings(model):
                       cost=1 + seed % 20)
             assert r["verdict"] == "ok", (ring, seed, r)
             assert r["lost"] == 0 and r["dup"] == 0
+
+
+@pytest.mark.parametrize("defer_lanes", [16, 32, 64])
+def test_end_split_terminates_and_conserves_paths(model, defer_lanes):
+    """The end-of-queue split (MM_END_SPLIT, A/B; policy bit 2): new chunks of
+    the queue's last 4 x waves chunks park all their live lanes once a wave has
+    seen the queue out, and claims made then take an even share of the ring.
+    Each new chunk parks this way at most once and every claim still runs >= 1
+    bounce: no deadlock, livelock, lost or duplicated path."""
+    end_parks = 0
+    for waves in (2, 4, 16):
+        for chunks in (1, 12, 24, 80):
+            for seed in range(1, 7):
+                r = model(waves, 64, 512, chunks, 20, defer_lanes, seed, policy=7, burst=1 + seed % 8,
+                          cost=1 + 7 * (seed % 4))
+                assert r["verdict"] == "ok", (waves, chunks, seed, r)
+                assert r["lost"] == 0 and r["dup"] == 0 and r["reserved"] == r["claimed"]
+                end_parks += r["end_parks"]
+    for ring in (4, 8, 16):
+        for seed in range(1, 21):
+            r = model(2 + seed % 5, 4, ring, 1 + seed % 9, 12, 1 + seed % 4, seed, policy=7, burst=1 + seed % 9,
+                      cost=1 + seed % 20)
+            assert r["verdict"] == "ok", (ring, seed, r)
+            assert r["lost"] == 0 and r["dup"] == 0
+            end_parks += r["end_parks"]
+    assert end_parks > 0  # the split path ran
