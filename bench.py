@@ -7,12 +7,18 @@ pixel x sample path traced through the HIP kernels (no work skipped), frame
 index = step number (fresh RNG every step).  A "ray" is one closest-hit BVH
 query (src/shaders.metal:307).
 
-N GPUs (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-the frame's rows are interleaved over ranks (rank r renders rows r, r+N, ...),
-and rank 0 receives every tile with one RCCL gather per frame, overlapped with
-the next frame's trace (north star:
-"tiles of the framebuffer shard one-per-GPU ... single RCCL gather at frame
-end").  Total work is fixed as N grows -> "scaling": "strong".
+N GPUs: one process per GPU.  `bench.py --gpus N` started on its own starts
+`python -m torch.distributed.run --nproc-per-node N bench.py <same args>` as a
+child and relays rank 0's line (so --gpus always means N GPUs); under a
+launcher (WORLD_SIZE set, as the driver runs it) WORLD_SIZE must equal --gpus.
+The frame's rows are interleaved over ranks (rank r renders rows r, r+N, ...),
+and rank 0 receives every rank's tiles with one RCCL gather per multi-frame
+launch through the library's C ABI (mm_gather_rows: ncclSend/ncclRecv + a
+de-interleave kernel, include/mm_comm.h), issued on its own stream (north
+star: "tiles of the framebuffer shard one-per-GPU ... single RCCL gather at
+frame end"); torch.distributed (gloo, on the CPU) carries only the
+rendezvous, barriers and the timing reductions.  Total work is fixed as N
+grows -> "scaling": "strong".
 
 Prints ONE JSON line on rank 0 (driver contract), with the roofline of the
 dominant kernel (HIP-event timed inside the timed region) and a CPU baseline
@@ -85,6 +91,9 @@ def usable_cpus():
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--launcher", default="auto", choices=["auto", "torchrun"],
+                   help="auto: N > 1 GPUs without a launcher start torchrun as a child; torchrun: also at N = 1 "
+                        "(the multi-GPU frame path -- RCCL communicator, gather -- on one rank)")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
@@ -115,6 +124,59 @@ def parse():
     p.add_argument("--save-frame", default="", help="rank 0 saves the last timed frame as it was delivered "
                                                     "(.npy; tests/test_gpu_rccl.py checks it)")
     return p.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(args, env, argv, port=None):
+    """How this invocation runs: ("run", None) in this process, ("child", cmd)
+    to start one process per GPU under torch.distributed.run (this script, the
+    same arguments), or ("error", message).  Decided before torch is imported
+    or any GPU is touched (--gpus N must mean N GPUs)."""
+    ws = env.get("WORLD_SIZE")
+    if args.gpus < 1:
+        return "error", f"--gpus {args.gpus}: need at least one GPU"
+    if ws is not None:
+        if int(ws) != args.gpus:
+            return "error", (f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={ws}: the GPU count and "
+                             f"the number of ranks must agree (one process per GPU)")
+        return "run", None
+    if args.gpus > 1 or args.launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()),
+               str(REPO / "bench.py")] + list(argv)
+        return "child", cmd
+    return "run", None
+
+
+def relay_child(cmd) -> int:
+    """Run the per-GPU ranks as a child process (never exec: see the harness
+    rules); rank 0's one JSON line goes to stdout, everything else to stderr.
+    Returns the exit status to leave with."""
+    import subprocess
+
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in p.stdout.splitlines():
+        try:
+            obj = json.loads(ln)
+        except ValueError:
+            obj = None
+        if isinstance(obj, dict) and "metric" in obj:
+            line = ln
+        elif ln.strip():
+            print(ln, file=sys.stderr)
+    if line is not None:
+        print(line, flush=True)
+    if p.returncode:
+        return p.returncode
+    return 0 if line is not None else 1
 
 
 def launch_sizes(count: int, per_launch: int) -> list:
@@ -293,6 +355,12 @@ def main():
     if args.src_hash:
         print(src_hash())
         return
+    how, what = launch_plan(args, os.environ, sys.argv[1:])
+    if how == "error":
+        print(f"bench.py: {what}", file=sys.stderr)
+        sys.exit(2)
+    if how == "child":
+        sys.exit(relay_child(what))
     # Exactly one JSON line on stdout: anything else written to fd 1 (e.g. the
     # RCCL banner at communicator init) is sent to stderr.
     json_out = os.fdopen(os.dup(1), "w")
@@ -307,12 +375,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # under torchrun (even with one rank) the frame goes through the RCCL gather path
+    # under torchrun (even with one rank) the frame goes through the RCCL gather path; torch.distributed (gloo,
+    # CPU) is only the rendezvous, the barriers and the timing reductions -- the frames move through the
+    # library's own RCCL communicator (include/mm_comm.h)
     distributed = "WORLD_SIZE" in os.environ and "MASTER_PORT" in os.environ
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist.init_process_group("gloo")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -339,9 +409,17 @@ def main():
         rens.append(r)
     streams = [r.own_stream() for r in rens]
     u = default_uniform(W, H, 0)
+    comm = None
+    if distributed:  # the library's RCCL communicator: rank 0's unique id over the gloo rendezvous
+        from mirror_maze.comm import Comm
+
+        uid = [Comm.unique_id(rens[0]) if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm.init_rank(rens[0], world, rank, uid[0])
 
     # rows r, r+world, ... (mirror_maze/dist.py); pad so every rank sends the same shape
-    from mirror_maze.dist import BatchGatherer, FrameGatherer, row_shard, rows_max
+    from mirror_maze.comm import NativeGatherer
+    from mirror_maze.dist import row_shard, rows_max
 
     y0, y_stride, my_rows = row_shard(H, world, rank)
     if args.emulate_ranks > 1 and world == 1:
@@ -350,23 +428,19 @@ def main():
     rgba8 = args.frame_format == "rgba8" and not args.accumulate
     fdt = torch.uint8 if rgba8 else torch.float32
     frame_buf = torch.empty((H, W, 4), dtype=fdt, device=dev) if rank == 0 else None
-    # one RCCL gather per frame, issued async on the frame's stream into
-    # rotating tiles so it overlaps later frames (mirror_maze/dist.py: FrameGatherer)
     # multi-frame launches need the wave-persistent kernel's fused resolve (64 % spp == 0)
     # (with the mirror-tail deferral -- MM_OPT_DEFER, or spp that does not divide 64 -- samples are staged per
     # frame, any spp)
     batchable = not args.accumulate
     fb_max = (min(args.batch, max(args.steps, args.warmup, 8)) if args.batch > 0 else 8) if batchable else 1
-    # gather slots: a batch's frames each need a slot whose previous gather (a batch earlier) is done,
-    # so the next launch never waits on this batch's own gathers
+    # ONE gather per launch (a multi-frame launch's frames all finish together; per frame with --batch 1),
+    # mm_gather_rows on its own stream into rotating tile slots, so the next launch never waits on it
+    # (mirror_maze.comm.NativeGatherer)
     asm_stream = torch.cuda.Stream(dev) if distributed else None
-    gatherer = (FrameGatherer((rows_max(H, world), W, 4), H, dev, out=frame_buf, dtype=fdt,
-                              slots=max(2, len(rens)), assembly_stream=asm_stream)
+    gatherer = (NativeGatherer(comm, (rows_max(H, world), W, 4), H, fb_max, dev, dtype=fdt,
+                               slots=max(2, len(rens)), gather_stream=asm_stream)
                 if distributed else None)
-    # multi-frame launches: ONE gather per launch (its frames all finish together)
-    bgather = (BatchGatherer((rows_max(H, world), W, 4), H, dev, fb_max, out=frame_buf, dtype=fdt, slots=2,
-                             assembly_stream=asm_stream)
-               if distributed and fb_max > 1 else None)
+    bgather = gatherer if distributed and fb_max > 1 else None
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=fdt, device=dev) for _ in rens]
     # float tiles the trace writes when the delivered frame is RGBA8 (one per context)
     ftiles = [torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev) for _ in rens] if rgba8 else None
@@ -401,7 +475,7 @@ def main():
                 if trace_end is not None:
                     trace_end[0].record(streams[slot])
                 return st
-            tile = gatherer.tile() if gatherer else tiles1[slot]
+            tile = gatherer.tiles(1)[0] if gatherer else tiles1[slot]
             ft = ftiles[slot] if rgba8 else tile
             _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
                                           y_stride=y_stride, out=ft[:my_rows], stats=stats)
@@ -410,7 +484,7 @@ def main():
             if rgba8:
                 rens[slot].quantize(ft[:my_rows], out=tile[:my_rows])
             if gatherer:
-                gatherer.put()
+                gatherer.put(1)
         last[0] = slot
         return st
 
@@ -458,26 +532,25 @@ def main():
     def gather_accumulated():
         with torch.cuda.stream(streams[0]):
             if gatherer:
-                gatherer.tile().copy_(acc_tile)
-                gatherer.put()
-                gatherer.flush()
+                gatherer.tiles(1)[0].copy_(acc_tile)
+                gatherer.put(1)
             else:
                 tiles1[0].copy_(acc_tile[:H])
                 last[0] = 0
 
     def flush_gathers():
-        if bgather:
-            bgather.flush()
-        if gatherer:
-            gatherer.flush()
+        return gatherer.flush() if gatherer else None
 
     def drain():
         if acc_tile is not None:
             gather_accumulated()
-        flush_gathers()
-        torch.cuda.synchronize(dev)
-        if not gatherer:
+        f = flush_gathers()  # rank 0's last delivered frame (the current stream waits for the gathers)
+        if gatherer is None:
+            torch.cuda.synchronize(dev)
             frame_buf.copy_(tiles1[last[0]])
+        elif f is not None:
+            frame_buf.copy_(f)
+        torch.cuda.synchronize(dev)
 
     if fb_max > 1 and args.batch > 1:  # warm up the issue mode that is timed
         active[0], batch[0] = len(rens), fb_max
@@ -506,7 +579,7 @@ def main():
                 t0 = time.perf_counter()
                 run_frames(0, 20_000 + 16 * rep, 8)
                 drain()
-                dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+                dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
                 if distributed:
                     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
                 calib[name] = min(calib.get(name, 1e9), float(dt.item()) / 8 * 1e3)
@@ -536,7 +609,7 @@ def main():
     assembled = None
     if distributed:  # the frame is on rank 0 (assembled) / this rank's gather done: exposed-gather clock
         assembled = torch.cuda.Event(enable_timing=True)
-        assembled.record(asm_stream if rank == 0 else torch.cuda.current_stream(dev))
+        assembled.record(asm_stream)
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -591,20 +664,24 @@ def main():
     torch.cuda.synchronize(dev)
     counter.close()
     assert ref_rays == rays or args.accumulate, (ref_rays, rays)
-    counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64, device=dev)
-    t_el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    counts = torch.tensor([rays, paths, visits, rtests], dtype=torch.float64)
+    t_el = torch.tensor([elapsed], dtype=torch.float64)
     dist_info = None
     if distributed:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_el, op=dist.ReduceOp.MAX)
         # per-rank kernel time and exposed gather (so a SCALE shortfall splits into trace imbalance vs gather)
-        k_lo = torch.tensor([k_ms, exposed_ms], dtype=torch.float64, device=dev)
+        k_lo = torch.tensor([k_ms, exposed_ms], dtype=torch.float64)
         k_hi = k_lo.clone()
         dist.all_reduce(k_lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(k_hi, op=dist.ReduceOp.MAX)
-        n_gathers = (bgather.launch if bgather else gatherer.k) if (bgather or gatherer) else 0
+        n_gathers = gatherer.launch
         dist_info = {
-            "rccl_world": dist.get_world_size(), "backend": str(dist.get_backend()),
+            "rccl_world": comm.n_ranks, "rccl_version": Comm.rccl_version(),
+            "backend": ("RCCL through libmirror_maze.so (mm_comm_init_rank + mm_gather_rows: ncclSend/ncclRecv "
+                        "to rank 0, de-interleave kernel); torch.distributed " + str(dist.get_backend()) +
+                        " for the rendezvous, barriers and timing reductions"),
+            "torch_distributed_world": dist.get_world_size(),
             "kernel_ms_per_rank": {"rank0": round(k_ms, 3), "min": round(float(k_lo[0]), 3),
                                    "max": round(float(k_hi[0]), 3)},
             "exposed_gather_ms": {"rank0": round(exposed_ms, 3), "max": round(float(k_hi[1]), 3),
@@ -668,6 +745,9 @@ def main():
             line["cpu_baseline"] = cpu_baseline(scene, u, make_ext(spp, bl, ml, frame=0), W, H, args.cpu_seconds)
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
+    if comm is not None:
+        torch.cuda.synchronize(dev)
+        comm.close()
     for r in rens:
         r.close()
     if distributed:

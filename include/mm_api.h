@@ -211,7 +211,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   rings' protocol waits give up at once (bit 2 when a wait was needed; a
                                   writer that gives up leaves NaN in its sample, mm_last_error names the
                                   first timed-out wait); 3 the trace call fails with MM_ERR_HIP after
-                                  taking its first launch's status slot, before the launch is enqueued */
+                                  taking its first launch's status slot, before the launch is enqueued;
+                                  4 the launch's first deferred path is lost (its ring entry is reserved,
+                                  never written): its reader times out after the normal bound and every
+                                  later protocol wait of the launch gives up within 256 polls */
 /* Default builds hold the kernels MM_PIPE_AUTO can select; values that need
  * the A/B-only variants (MM_OPT_PERSIST 0, MM_OPT_TRAVERSAL 0,
  * MM_OPT_LDS_SPLIT > 1, MM_OPT_DICT_NODES 2, BVH form 7 without nodes +

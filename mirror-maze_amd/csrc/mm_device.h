@@ -146,7 +146,6 @@ __device__ __forceinline__ float dot3(F3 a, F3 b) {
 // IEEE expansion.
 __device__ __forceinline__ float rsq_ieee(float x) { return 1.0f / sqrtf(x); }
 __device__ __forceinline__ float rsq(float x) {
-#ifndef MM_NO_FAST_RSQ
     if (x >= 0x1p-40f && x <= 0x1p40f) {
         float s = __builtin_amdgcn_sqrtf(x);
         const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
@@ -157,7 +156,6 @@ __device__ __forceinline__ float rsq(float x) {
         const float e = __builtin_fmaf(-s, y, 1.0f);
         return __builtin_fmaf(e, y, y);
     }
-#endif
     return rsq_ieee(x);
 }
 __device__ __forceinline__ F3 normalize3(F3 v) { return rsq(dot3(v, v)) * v; }
@@ -176,11 +174,7 @@ __device__ __forceinline__ float rand_pm1(uint32_t& state) {
     r = (r >> 22) ^ r;
     // RN(RN(float(r) * 2^-31) - 1): the product is exact (a power-of-two
     // scaling of a float in [1, 2^32]), so one fma rounds the same once
-#ifdef MM_NO_FMA_RAND
-    return (float)r * 0x1p-31f - 1.0f;
-#else
     return __builtin_fmaf((float)r, 0x1p-31f, -1.0f);
-#endif
 }
 
 // air.convert.u.i32.f.f32: truncation, saturating, NaN -> 0

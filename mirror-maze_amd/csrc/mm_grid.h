@@ -147,11 +147,7 @@ __device__ __forceinline__ void grid_rect(const GV& gv, const float4* __restrict
         }
     }
     const uint32_t ak = (meta >> 20) & 3u;
-#ifdef MM_NO_XZ_SELECT
-    constexpr bool kTwoWay = false;
-#else
     constexpr bool kTwoWay = kXZ;
-#endif
     // compact (maze) records: x or z normal, y the first in-plane axis
     // (grid_build.cpp), so k0 is one compare and (v, u) = (y, the other)
     const bool k0 = kCompact ? meta < (1u << 20) : ak == 0u, k2 = kTwoWay ? !k0 : ak == 2u;
@@ -200,9 +196,6 @@ __device__ __forceinline__ void grid_rect_axis(const GV& gv, uint32_t k, uint4 w
 template <bool kSlow, bool kCompact, typename GV>
 __device__ __forceinline__ void grid_rect_uniform(const GV& gv, const float4* __restrict__ geo, uint32_t k,
                                                   const Ray& r, float& best, uint32_t& bk, uint32_t& tie) {
-#ifdef MM_NO_UNIFORM_GLOBALS  // A/B: the per-lane selecting test
-    grid_rect<kSlow, false, kCompact>(gv, geo, k, r, best, bk, tie);
-#else
     const uint4 w = rec_words<kCompact>(gv, k);
     const uint32_t meta = __builtin_amdgcn_readfirstlane(w.w);
     if (kSlow && (meta >> 30) == 2u) {
@@ -213,7 +206,6 @@ __device__ __forceinline__ void grid_rect_uniform(const GV& gv, const float4* __
     if (ak == 0u) grid_rect_axis<0, kCompact>(gv, k, w, r, best, bk, tie);
     else if (ak == 1u) grid_rect_axis<1, kCompact>(gv, k, w, r, best, bk, tie);
     else grid_rect_axis<2, kCompact>(gv, k, w, r, best, bk, tie);
-#endif
 }
 
 // (&=, not &&: see ray_fast_ok)
@@ -260,7 +252,6 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     float best = kBig;
     uint32_t bk = 0xFFFFFFFFu;
     uint32_t tie = 0u;  // (a bool lives in an exec-mask register: SALU merges at every join)
-#ifndef MM_NO_SLAB_GLOBALS
     // Floor and ceiling (g.slab): a y-normal plane the ray moves away from
     // gives a = RN(num / d_y) with num = RN(Y - o_y) on the wrong side of
     // RN(0.05 d_y), so a <= 0.05 (1 + u) and a > 0.1 fails -- that rect
@@ -284,12 +275,6 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
         }
     }
-#else
-    for (uint32_t j = 0; j < g.n_glob; ++j) {
-        MM_LANE_STAT(kLpGlobal);
-        grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
-    }
-#endif
     // The walk starts in the cell of the ray's point at t = 3/32, not at the
     // origin: a rect of A has a > 0.1, so the cells the ray occupies only for
     // t < 3/32 hold nothing it can return, and the rounding of the start
@@ -304,7 +289,6 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     int bx = grid_first(g, 0, r.o.x + s0 * r.d.x, r.y.x),
         by = kFlat ? (r.y.y > 0.0f ? 1 : 0) : grid_first(g, 1, r.o.y + s0 * r.d.y, r.y.y),
         bz = grid_first(g, 2, r.o.z + s0 * r.d.z, r.y.z);
-#ifndef MM_DIRECT_CELL_TIME
     // Crossing time of boundary b along axis a in one fma per step:
     // t = RN(b * B_a + A_a), A_a = RN(RN(mn_a - o_a) * y_a), B_a = RN(cell_a * y_a).
     // Its error along axis a, |dt| * |d_a|, is a few u (|mn_a - o_a| + b cell_a
@@ -316,10 +300,6 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     const float Ay = kFlat ? 0.0f : (g.mn[1] - r.o.y) * r.y.y, By = kFlat ? 0.0f : g.cell[1] * r.y.y;
     float tx = __builtin_fmaf((float)bx, Bx, Ax), tz = __builtin_fmaf((float)bz, Bz, Az);
     float ty = kFlat ? grid_time(g, 1, by, r.o.y, r.y.y) : __builtin_fmaf((float)by, By, Ay);
-#else
-    float tx = grid_time(g, 0, bx, r.o.x, r.y.x), ty = grid_time(g, 1, by, r.o.y, r.y.y),
-          tz = grid_time(g, 2, bz, r.o.z, r.y.z);
-#endif
     // Cell words (grid_build.cpp).  Wide (64-bit): bits 0-21 the list's first
     // entry; bit 63 set: bits 22-31 the count, the whole list for every face;
     // clear: bits 22-24 the count m <= 7, and per entry face f a 6-bit
@@ -327,7 +307,6 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // across f did not already hold.  Plain (32-bit): first | count << 22.
     // face = 6: the whole list (the first cell).  (A run-time format flag
     // cost 2 % on C3: the format is a template parameter.)
-#ifndef MM_NO_STEP_CELL
     // The current cell's index, stepped with the walk (+-1 per x step, +-n0 per
     // z step (n0 n1 in 3-D), +-n0 per y step), and the bit offset of each
     // axis's entry-face field in the wide cell word (25 + 6 f; the face
@@ -360,31 +339,8 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             j1 = j0 + (cw >> 22);
         }
     };
-#else
-    auto cell_range = [&](uint32_t face, uint32_t& j0, uint32_t& j1) {
-        const int ix = r.y.x > 0.0f ? bx - 1 : bx, iz = r.y.z > 0.0f ? bz - 1 : bz;
-        const int iy = kFlat ? 0 : (r.y.y > 0.0f ? by - 1 : by);
-        const uint32_t c = kFlat ? (uint32_t)(iz * g.n[0] + ix) : (uint32_t)((iz * g.n[1] + iy) * g.n[0] + ix);
-        if constexpr (kWide) {
-            const uint64_t cw = reinterpret_cast<const uint64_t*>(gv.cells)[c];
-            const bool whole = (cw >> 63) != 0;
-            const uint32_t m = (uint32_t)(cw >> 22) & (whole ? 0x3FFu : 7u);
-            const uint32_t fld = face < 6u ? (uint32_t)(cw >> (25u + 6u * face)) & 63u : (m << 3);
-            j0 = ((uint32_t)cw & 0x3FFFFFu) + (whole ? 0u : (fld & 7u));
-            j1 = j0 + (whole ? m : (fld >> 3));
-        } else {
-            const uint32_t cw = reinterpret_cast<const uint32_t*>(gv.cells)[c];
-            j0 = cw & 0x3FFFFFu;
-            j1 = j0 + (cw >> 22);
-        }
-    };
-#endif
     uint32_t j, jend;
-#ifndef MM_NO_STEP_CELL
     cell_range(0u, j, jend);
-#else
-    cell_range(6u, j, jend);
-#endif
     uint32_t cells = 1, tests = g.n_glob;
     // One iteration: test one rect of the current cell; when the cell's list
     // is done, step to the next cell (or stop) in the same iteration.
@@ -415,24 +371,12 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             // (by-value selects: a select of two loads becomes a load of a
             // selected address -- of the kernel argument or a scratch copy)
             const int b = sx ? bx : (sy ? by : bz);
-            [[maybe_unused]] const float ya = sel_xy(sx, sy, r.y);
-#ifndef MM_DIRECT_CELL_TIME
             const float nt = __builtin_fmaf((float)b, sel_xy(sx, sy, F3{Bx, By, Bz}), sel_xy(sx, sy, F3{Ax, Ay, Az}));
-#else
-            const float mn = sel_xy(sx, sy, F3{g.mn[0], g.mn[1], g.mn[2]});
-            const float cs = sel_xy(sx, sy, F3{g.cell[0], g.cell[1], g.cell[2]});
-            const float oa = sel_xy(sx, sy, r.o);
-            const float nt = ((mn + (float)b * cs) - oa) * ya;
-#endif
             tx = sx ? nt : tx;
             ty = sy ? nt : ty;
             tz = sz ? nt : tz;
-#ifndef MM_NO_STEP_CELL
             ci += sx ? dcx : (sy ? dcy : dcz);
             cell_range((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu, j, jend);
-#else
-            cell_range((sx ? 0u : (sy ? 2u : 4u)) + (ya > 0.0f ? 0u : 1u), j, jend);  // (ya: by value, see above)
-#endif
             if (kStats) ++cells;
         }
     }

@@ -77,13 +77,14 @@ struct TileJob {
     // (host-mapped; trace_kernels.hip ring_timeout); launch_id goes into it.
     uint32_t* ring_diag = nullptr;
     uint32_t launch_id = 0;
-    // MM_OPT_FAULT_INJECT 1: the launch raises error bit 3 (tests of the
-    // error path).
+    // MM_OPT_FAULT_INJECT 1: the launch raises error bit 3; 4: its first
+    // deferred path is lost (bit 4, and the reader's ring timeout) -- tests of
+    // the error path.
     uint32_t fault = 0;
 };
 
 // Error flag bits (aux word 4, and the status word's low bits).
-constexpr uint32_t kErrStack = 1u, kErrRing = 2u, kErrInjected = 8u;
+constexpr uint32_t kErrStack = 1u, kErrRing = 2u, kErrInjected = 8u, kErrLost = 16u, kErrPublish = 32u;
 constexpr uint32_t kStatusDone = 0x80000000u;
 
 // One-thread kernel that publishes a non-persistent launch's error flag into

@@ -21,6 +21,7 @@
 
 #include "grid_build.h"
 #include "mm_api.h"
+#include "mm_ctx.h"
 #include "mm_launch.h"
 
 using namespace mm;
@@ -29,103 +30,6 @@ namespace mm {
 size_t build_compact_rects(const mm_rect* rects, uint32_t n_rects, const uint32_t* idx, std::vector<uint32_t>& out,
                            size_t* n_slow);
 }
-
-struct mm_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-    // scene (buffers 1,2,3,5,6 of compute_shader)
-    mm_rect* d_rects = nullptr;
-    float4* d_nodes = nullptr;      // production layout (packed child words)
-    float4* d_nodes_ref = nullptr;  // reference layout
-    uint32_t root_packed = 0;
-    bool fast_ok = false;
-    uint32_t depth = 0;         // tree depth = max traversal stack entries
-    float4* d_geo = nullptr;
-    float4* d_shade = nullptr;
-    uint2* d_recs = nullptr;    // compact leaf-ordered rect records
-    size_t n_fast_recs = 0;
-    bool lean_ok = false;       // no SLOW rect records (loop form 7, grid search)
-    float* d_dict_tab = nullptr;       // dictionary-coded nodes (mode 10): 256 values
-    uint32_t* d_dict_words = nullptr;  // 3 words per production node
-    bool dict_ok = false;
-    uint8_t* d_grid = nullptr;  // certified grid search (grid_build.cpp, mm_grid.h)
-    DevGrid grid{};
-    bool grid_ok = false;
-    bool grid_slow = false;  // the grid has SLOW records (general rect test)
-    bool grid_wide = false;  // 64-bit cell words with per-face list ranges
-    bool grid_flat = false;  // the flat forms apply (grid_build.h GridHost::flat_ok)
-    std::string grid_why;
-    uint32_t* d_idx = nullptr;
-    uint32_t n_rects = 0, n_nodes = 0;
-    bool has_scene = false;
-    // texout (parity mode)
-    float4* d_fb = nullptr;
-    uint32_t* d_fb8 = nullptr;
-    uint32_t* d_fb8_alt = nullptr;  // presentation blur target (swapped with d_fb8)
-    uint32_t last_chunks = 0;       // chunk count of the last mm_trace_chunks
-    float4* d_packets = nullptr;
-    size_t packets_cap = 0;
-    uint32_t fb_w = 0, fb_h = 0;
-    // chunk list (buffer 0)
-    uint32_t* d_chunks = nullptr;
-    size_t chunks_cap = 0;
-    // per-sample staging (throughput mode)
-    float4* d_samples = nullptr;
-    size_t samples_cap = 0;
-    // mirror-tail rings' records (MM_OPT_DEFER)
-    void* d_tail = nullptr;
-    uint32_t tail_cap = 0;
-    // aux: stats[4] (u64) + error flag (u32)
-    unsigned long long* d_aux = nullptr;
-    uint32_t* d_work = nullptr;  // the wave-persistent kernel's self-cleaning queue heads + waves-done word (4 KB)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    float last_ms = 0.0f;
-    uint32_t last_launches = 0;
-    int pipe = MM_PIPE_AUTO;
-    // options (include/mm_api.h MM_OPT_*); defaults = the measured fastest
-    bool opt_lds = true;            // stage scene data in LDS where it fits
-    uint32_t opt_block = 0;         // k_trace_mega block size (0 = auto)
-    int opt_persist = 2;            // 0 one thread per path (k_trace_mega), 2 wave-persistent
-    int opt_ww = -1;                // loop form: -1 auto, 0, 5, 7 (BVH), 11 (grid search)
-    int opt_lds_rects = 1;          // compact rect records in LDS beside the nodes when they fit
-    uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto, else KB (always)
-    bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
-    uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
-    uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
-    int opt_defer = -1;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off, -1 auto)
-    uint32_t opt_defer_min = 1u << 24;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
-    int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
-    unsigned long long* d_wave_ts = nullptr;  // diagnostics (mm_set_wave_timeline)
-    uint32_t wave_ts_cap = 0;
-    // per-kernel profiling of the trace kernel (mm_set_profiling)
-    bool prof = false;
-    std::vector<hipEvent_t> prof_ev;   // pairs (start, stop)
-    size_t prof_used = 0;              // events recorded since last reset
-    // Per-launch status words (host-mapped pinned memory): launch L of the
-    // context writes slot L % kStatusSlots when it ends (error bits |
-    // kStatusDone).  Each mm_trace_tile* call is a numbered "call" owning a
-    // run of launches; a call whose launches raised an error is reported,
-    // naming the call, by the next call on the context, mm_sync or
-    // mm_call_status -- never blamed on a later call's work.
-    uint32_t* h_status = nullptr;
-    uint32_t* d_status = nullptr;
-    std::vector<uint64_t> slot_owner;  // launch id + 1 holding each slot, 0 = free
-    uint64_t launch_seq = 0, call_seq = 0;
-    struct Call { uint64_t id, first, n; std::string what; uint32_t bits; };
-    struct Failed { uint64_t id; uint32_t bits; std::string what; bool reported; };
-    std::deque<Call> pending;
-    std::deque<Failed> failed;  // the last kFailedKept failed calls
-    uint64_t failed_dropped = 0;  // highest call id dropped from `failed` (older ids: status no longer kept)
-    int opt_fault = 0;           // MM_OPT_FAULT_INJECT
-    bool opt_grid_merge = true;  // MM_OPT_GRID_MERGE (read by mm_upload_scene)
-    int opt_grid_cell = 100;     // MM_OPT_GRID_CELL (read by mm_upload_scene)
-    bool opt_grid_wide = true;   // MM_OPT_GRID_WIDE (read by mm_upload_scene)
-    bool last_defer = false;     // the last trace call ran the tail rings
-    int last_kern_mode = -1, last_kern_form = -1;  // for MM_INFO_LAST_VGPRS / _SCRATCH
-    int last_kern_ring = 0;      // its tail-ring kind (wavepersist_attributes: 0 none, 1 global, 2 LDS records)
-};
 
 constexpr uint32_t kStatusSlots = 1024;
 constexpr uint32_t kRingDiagWords = 16;  // after the status words: the first timed-out ring wait's record
@@ -137,10 +41,7 @@ constexpr uint64_t kStagePathsMax = 1ull << 29;
 
 namespace {
 
-int fail(mm_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
-    return code;
-}
+int fail(mm_ctx* c, int code, const std::string& msg) { return ctx_fail(c, code, msg); }
 
 #define HIPC(ctx, expr)                                                                           \
     do {                                                                                          \
@@ -310,13 +211,22 @@ int next_status(mm_ctx* c, uint32_t*& dev_word) {
     return MM_OK;
 }
 
-// The record the launch's first timed-out ring wait left (trace_kernels.hip
-// ring_timeout), as text; consumed (a later trip writes a new one).
-std::string ring_diag_text(mm_ctx* c) {
+// The record a timed-out ring wait left (trace_kernels.hip ring_timeout), as
+// text, when it belongs to one of the launches [first, first + n) of the call
+// being reported; consumed then (the device writes a new record only into a
+// consumed one).  A record of an older launch than the call's is stale (its
+// call was reported without it) and is dropped; a newer one is left for its
+// own call.
+std::string ring_diag_text(mm_ctx* c, uint64_t first, uint64_t n) {
     uint32_t* d = c->h_status + kStatusSlots;
-    if (!__atomic_load_n(d, __ATOMIC_ACQUIRE)) return "";
+    if (__atomic_load_n(d, __ATOMIC_ACQUIRE) != 1u) return "";  // none, or being written (2)
     uint32_t w[kRingDiagWords];
     for (uint32_t i = 0; i < kRingDiagWords; ++i) w[i] = __atomic_load_n(d + i, __ATOMIC_RELAXED);
+    const uint32_t rel = w[15] - (uint32_t)first;  // launch ids are the context's launch numbers, mod 2^32
+    if (rel >= (uint32_t)n) {
+        if ((int32_t)rel < 0) __atomic_store_n(d, 0u, __ATOMIC_RELEASE);  // stale: free the record
+        return "";
+    }
     const uint64_t t1 = w[12] | (uint64_t)w[13] << 32;
     char b[320];
     snprintf(b, sizeof(b),
@@ -328,12 +238,14 @@ std::string ring_diag_text(mm_ctx* c) {
     return b;
 }
 
-std::string error_text(mm_ctx* c, uint32_t bits) {
+std::string error_text(mm_ctx* c, uint32_t bits, uint64_t first, uint64_t n) {
     std::string s;
     auto add = [&](const std::string& m) { s += s.empty() ? m : std::string("; ") + m; };
     if (bits & kErrStack) add("traversal stack overflow (depth > 50)");
-    if (bits & kErrRing) add("tail ring wait timed out (kernel protocol error)" + ring_diag_text(c));
+    if (bits & kErrRing) add("tail ring wait timed out (kernel protocol error)" + ring_diag_text(c, first, n));
     if (bits & kErrInjected) add("injected fault (MM_OPT_FAULT_INJECT)");
+    if (bits & kErrLost) add("injected lost tail-ring entry (MM_OPT_FAULT_INJECT 4)");
+    if (bits & kErrPublish) add("the launch's status could not be published (its error flag was read after a sync)");
     return s.empty() ? "unknown error" : s;
 }
 int error_code(uint32_t bits) { return (bits & ~kErrStack) ? MM_ERR_HIP : MM_ERR_STACK; }
@@ -352,7 +264,7 @@ void poll_calls(mm_ctx* c) {
         }
         if (!done) { ++it; continue; }
         if (bits) {
-            c->failed.push_back({it->id, bits, it->what + " -- " + error_text(c, bits), false});
+            c->failed.push_back({it->id, bits, it->what + " -- " + error_text(c, bits, it->first, it->n), false});
             if (c->failed.size() > kFailedKept) {
                 c->failed_dropped = std::max(c->failed_dropped, c->failed.front().id);
                 c->failed.pop_front();
@@ -436,6 +348,7 @@ void mm_destroy(mm_ctx* c) {
     (void)hipFree(c->d_fb); (void)hipFree(c->d_fb8); (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_tail); (void)hipFree(c->d_work);
+    (void)hipFree(c->d_gather);
     if (c->h_status) (void)hipHostFree(c->h_status);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -525,7 +438,7 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             c->opt_grid_cell = value;
             return MM_OK;
         case MM_OPT_FAULT_INJECT:
-            if (value < 0 || value > 3) return fail(c, MM_ERR_INVALID, "fault inject must be 0..3");
+            if (value < 0 || value > 4) return fail(c, MM_ERR_INVALID, "fault inject must be 0..4");
             c->opt_fault = value;
             return MM_OK;
         default: return fail(c, MM_ERR_INVALID, "unknown option");
@@ -1049,7 +962,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
         job.n_frames = n_frames;
         job.reserve_cus = c->opt_reserve_cus;
-        job.fault = c->opt_fault == 1 ? 1u : 0u;
+        job.fault = (c->opt_fault == 1 || c->opt_fault == 4) ? (uint32_t)c->opt_fault : 0u;
         if (c->opt_fault == 2) job.ring_spin = 0;
         if (defer) {
             job.defer_from = 1;
@@ -1085,7 +998,19 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
                 mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
                 HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux, err_dev, want_stats, mo,
                                           c->stream));
-                HIPC(c, launch_publish_status(err_dev, job.status, c->stream));
+                enqueued = true;  // the kernel runs: its slot is written by the publish below or here
+                const hipError_t pe = launch_publish_status(err_dev, job.status, c->stream);
+                if (pe != hipSuccess) {
+                    // fold the kernel's error flag into THIS launch's slot (after a sync), so it is
+                    // never published by -- and blamed on -- a later call's launch
+                    uint32_t bits = 0;
+                    (void)hipStreamSynchronize(c->stream);
+                    (void)hipMemcpy(&bits, err_dev, sizeof(bits), hipMemcpyDeviceToHost);
+                    (void)hipMemset(err_dev, 0, sizeof(bits));
+                    __atomic_store_n(c->h_status + (c->launch_seq - 1) % kStatusSlots,
+                                     bits | kErrPublish | kStatusDone, __ATOMIC_RELEASE);
+                    return fail(c, MM_ERR_HIP, std::string("launch_publish_status: ") + hipGetErrorString(pe));
+                }
             }
             enqueued = true;
             return prof_mark(c);

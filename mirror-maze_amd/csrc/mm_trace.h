@@ -46,13 +46,9 @@ struct Ray {
 // (scripts/verify_fast_rsq.hip checks every float of either sign in
 // [2^-44, 2^44]); outside, the value is never used.
 __device__ __forceinline__ float rcp_guarded(float d) {
-#ifdef MM_NO_FAST_RCP
-    return 1.0f / d;
-#else
     const float y = __builtin_amdgcn_rcpf(d);
     const float e = __builtin_fmaf(-d, y, 1.0f);
     return __builtin_fmaf(e, y, y);
-#endif
 }
 
 __device__ __forceinline__ Ray make_ray(F3 o, F3 d) {

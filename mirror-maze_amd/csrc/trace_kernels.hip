@@ -325,11 +325,18 @@ __device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
 // timeout (100 MHz), [14] polls, [15] launch id.  (No clock at the wait's
 // start: a 64-bit value live across the wait loop cost the deferral kernel
 // 10 more scratch operations in its chunk loop; the polls give the length.)
+// [0] is taken by a compare-and-swap 0 -> 2 before the fields are written and
+// set to 1 after: a record the host has not read yet (1) is never overwritten
+// by a later launch's timeout, and the host reads only 1.
 __device__ __forceinline__ void ring_timeout(const TileJob& job, uint32_t* err, uint32_t role, uint32_t seq,
                                              uint32_t want, uint32_t seen, uint32_t polls) {
     if (atomicOr(err, kErrRing) & kErrRing) return;  // not the launch's first timeout
     uint32_t* d = job.ring_diag;
     if (!d) return;
+    uint32_t free_word = 0u;
+    if (!__hip_atomic_compare_exchange_strong(d, &free_word, 2u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM))
+        return;  // an earlier launch's record is still unread
     const uint64_t t1 = wall_clock64();
     d[1] = role; d[2] = seq; d[3] = want; d[4] = seen;
     d[5] = lds_ld(ring_ctl() + 0); d[6] = lds_ld(ring_ctl() + 1);
@@ -350,6 +357,14 @@ __device__ __forceinline__ bool ring_wait(uint32_t seq, uint32_t c, uint32_t rol
             ring_timeout(job, err, role, seq, want, seen, i);
             return false;
         }
+        // Once a wait of this launch has timed out (error bit 2) the turn words no longer
+        // describe the ring: a reader that gave up never releases its slot's next lap, a
+        // writer that gave up never releases its entry.  Every later wait gives up within
+        // 256 polls instead of spinning the whole bound, so one protocol slip ends the
+        // launch in milliseconds, not in (waits x 50 ms) -- ADVICE r04.
+        if ((i & 255u) == 255u &&
+            (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kErrRing))
+            return false;
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -378,13 +393,12 @@ constexpr uint32_t kClaimTail = MM_CLAIM_TAIL;  // single claims for the last kC
 #ifdef MM_TAIL_CLOCKS
 constexpr uint32_t kClaimWords = 16;
 #else
-constexpr uint32_t kClaimWords = 3;
+constexpr uint32_t kClaimWords = 2;
 #endif
 __device__ __forceinline__ uint32_t* claim_words() {
-    // (next, end, head) per wave of a <= 1024-thread block (head: MM_XCD_HEADS, the queue head the wave
-    // pulls from); diagnostics build MM_TAIL_CLOCKS: then the wall clock at the start of the wave's current
-    // chunk (lo, hi), its longest chunk so far (10 ns units), its chunks over 100 us, the clock when it saw
-    // the global queue out (lo, hi)
+    // (next, end) per wave of a <= 1024-thread block; diagnostics build MM_TAIL_CLOCKS: then the wall clock
+    // at the start of the wave's current chunk (lo, hi), its longest chunk so far (10 ns units), its chunks
+    // over 100 us, the clock when it saw the global queue out (lo, hi)
     __shared__ uint32_t w[kClaimWords * 16];
     return w + kClaimWords * (threadIdx.x >> 6);
 }
@@ -426,114 +440,24 @@ __device__ __forceinline__ void mark_queue_out(const TileJob& job) {
 __device__ __forceinline__ void claim_reset() {
     if ((threadIdx.x & 63u) == 0) {
         for (uint32_t i = 0; i < kClaimWords; ++i) claim_words()[i] = 0u;
-#ifdef MM_XCD_HEADS
-        claim_words()[2] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // hwreg(HW_REG_XCC_ID, 0, 4): 0-7
-#endif
     }
 }
-// Progress-fair wave priority (MM_FAIR_PRIO, A/B): the SIMD's arbiter favours older waves, and in a
-// persistent launch the oldest waves of a SIMD take several times the chunks of the youngest (C3: 184 to
-// 1,523 chunks per wave, profiles/r04/tail_probe_*.txt); at the queue's end the young waves are then still
-// several of their (long) chunks from done.  Each claim sets the wave's priority from how far it is
-// behind the chip's mean chunks per wave (head / 64 / waves), so the waves finish together.
-__device__ __forceinline__ void fair_prio(uint32_t head, uint32_t chunks_done) {
-#ifdef MM_FAIR_PRIO
-    const uint32_t mean = head / (64u * gridDim.x * (blockDim.x >> 6));
-    if (chunks_done + 8u < mean) __builtin_amdgcn_s_setprio(3);
-    else if (chunks_done + 4u < mean) __builtin_amdgcn_s_setprio(2);
-    else if (chunks_done < mean) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-#else
-    (void)head; (void)chunks_done;
-#endif
-}
-// End-of-queue priority (MM_END_PRIO=z, A/B): the last waves out are their SIMD's youngest (launch
-// order 7 of 8 in 123 of the last 163; profiles/r04/tail_probe/tail_probe_simd.txt), whose chunks run
-// at a seventh of the oldest's rate until the old waves exit.  From the last z x (waves x claim) paths
-// of the queue on, each chunk start sets the wave's priority from its deficit against the chip's mean
-// chunks per wave, so a SIMD's waves finish their last chunks together.
-__device__ __forceinline__ void end_prio(uint32_t next, uint32_t n_queue, uint32_t chunks_done) {
-#ifdef MM_END_PRIO
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    const uint32_t zone = MM_END_PRIO * waves * kClaimChunks * 64u;
-    if (next < n_queue && (n_queue <= zone || next >= n_queue - zone)) {
-        const uint32_t mean = next / (64u * waves);
-        if (2u * chunks_done < mean) __builtin_amdgcn_s_setprio(3);
-        else if (4u * chunks_done < 3u * mean) __builtin_amdgcn_s_setprio(2);
-        else if (chunks_done < mean) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-    }
-#else
-    (void)next; (void)n_queue; (void)chunks_done;
-#endif
-}
-
-#ifndef MM_XCD_HEADS
 constexpr uint32_t kDoneWord = 1;  // work[0] = next path, work[1] = waves done
-__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue, uint32_t chunks_done) {
+__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
     uint32_t* cw = claim_words();
     uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
     if (next >= end) {
         const uint32_t big = kClaimChunks * 64u;
         const uint32_t tail = kClaimTail * gridDim.x * (blockDim.x >> 6) * big;  // below: single claims
         const uint32_t k = (n_queue > tail && next < n_queue - tail) ? big : 64u;
-#ifdef MM_TAIL_RETIRE
-        // (A/B) in the single-claim zone a wave that has done under half the chip's mean chunks takes no
-        // more: its next chunk would be among the last to finish
-        if (k == 64u && next > 0u && chunks_done < next / (128u * gridDim.x * (blockDim.x >> 6))) {
-            if ((threadIdx.x & 63u) == 0) { cw[0] = n_queue + 64u; cw[1] = n_queue; }
-            return n_queue;
-        }
-#endif
         uint32_t b = 0;
         if ((threadIdx.x & 63u) == 0) b = atomicAdd(work, k);
         next = __builtin_amdgcn_readfirstlane(b);
         end = min(next + k, n_queue);
-        fair_prio(next, chunks_done);
-    }
-    end_prio(next, n_queue, chunks_done);
-    if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
-    return next;
-}
-#else
-// Per-XCD queue heads (MM_XCD_HEADS; MI355X_MICROARCH.md "dequeue": one head word saturates at ~88
-// dequeues/us, shard it above 64 pullers): the queue's chunks are dealt to 8 heads in contiguous eighths,
-// head h at work[h * kHeadStride]; a wave pulls from its XCD's head (HW_REG_XCC_ID) and, once that is out,
-// from the next ones in turn; the queue is out when all 8 are.  kClaimChunks chunks per claim down to the
-// head's last kClaimTail x (its waves x claim) paths, then single chunks.
-constexpr uint32_t kHeadStride = 32;              // 128 B apart
-constexpr uint32_t kDoneWord = 8 * kHeadStride;  // waves done
-__device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue, uint32_t chunks_done) {
-    (void)chunks_done;
-    uint32_t* cw = claim_words();
-    uint32_t next = __builtin_amdgcn_readfirstlane(cw[0]), end = __builtin_amdgcn_readfirstlane(cw[1]);
-    if (next >= end) {
-        const uint32_t per = ((n_queue / 64u + 7u) / 8u) * 64u;  // paths per head
-        const uint32_t big = kClaimChunks * 64u;
-        const uint32_t tail = kClaimTail * (gridDim.x * (blockDim.x >> 6) / 8u) * big;
-        uint32_t h = __builtin_amdgcn_readfirstlane(cw[2]);
-        next = end = n_queue;
-        for (uint32_t tries = 0; tries < 8u; ++tries, h = (h + 1u) & 7u) {
-            const uint32_t lo = min(h * per, n_queue), hi = min(lo + per, n_queue);
-            if (lo >= hi) continue;
-            const uint32_t last = __builtin_amdgcn_readfirstlane(cw[0]);
-            const uint32_t done = last >= lo && last <= hi ? last - lo : 0u;  // where this wave last claimed here
-            const uint32_t k = (per > tail && done < per - tail) ? big : 64u;
-            uint32_t b = 0;
-            if ((threadIdx.x & 63u) == 0) b = atomicAdd(work + h * kHeadStride, k);
-            b = __builtin_amdgcn_readfirstlane(b);
-            if (b < hi - lo) {
-                next = lo + b;
-                end = min(next + k, hi);
-                break;
-            }
-        }
-        if ((threadIdx.x & 63u) == 0) cw[2] = h;
     }
     if ((threadIdx.x & 63u) == 0) { cw[0] = next + 64u; cw[1] = end; }
     return next;
 }
-#endif
 
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
@@ -550,7 +474,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
     uint32_t paths = 0, chunks = 0;
     claim_reset();
     for (;;) {
-        const uint32_t base = dequeue(work, n_queue, chunks);
+        const uint32_t base = dequeue(work, n_queue);
         if (base >= n_queue) {
             mark_queue_out(job);
             break;
@@ -656,7 +580,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
 #endif
                 continue;
             }
-            b = dequeue(work, n_queue, chunks);
+            b = dequeue(work, n_queue);
             if (b >= n_queue) {
                 defer_from = 1 << 30;
                 mark_queue_out(job);
@@ -713,7 +637,11 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
                 df, job.defer_lanes, [&]() { return ring_reserve(seq); });
             if (overflow) atomicOr(err, kErrStack);
             if (deferred) {
-                if (ring_wait(seq, 0u, 2u, job, err)) {
+                // MM_OPT_FAULT_INJECT 4 (tests): the launch's first deferred path is lost -- its entry
+                // is reserved but never written, so its reader's wait times out
+                if (job.fault == 4u && !(atomicOr(err, kErrLost) & kErrLost)) {
+                    poison(samples, slot, n_slots);
+                } else if (ring_wait(seq, 0u, 2u, job, err)) {
                     tail_store<kLdsPay>(tq, seq % kTailRing, p, slot);
                     __hip_atomic_store(ring_turn(seq), ring_turn_value(seq, 1u), __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -909,11 +837,7 @@ __device__ __forceinline__ void persistent_exit(const TileJob& job, uint32_t chu
         __threadfence();
         const uint32_t total = gridDim.x * (blockDim.x >> 6);
         if (atomicAdd(counter + kDoneWord, 1u) == total - 1) {
-#ifdef MM_XCD_HEADS
-            for (uint32_t h = 0; h < 8u; ++h) atomicExch(counter + h * kHeadStride, 0u);
-#else
             atomicExch(counter, 0u);
-#endif
             atomicExch(counter + kDoneWord, 0u);
             if (job.status) {
                 const uint32_t e = atomicExch(err, 0u);

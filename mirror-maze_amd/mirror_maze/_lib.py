@@ -46,6 +46,7 @@ MM_INFO_LAST_DEFER, MM_INFO_LAST_VGPRS, MM_INFO_LAST_SCRATCH, MM_INFO_LAST_STATI
 MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
+MM_COMM_ID_BYTES, MM_GATHER_SELF_VIA_RCCL = 128, 1
 
 
 class mm_rect(C.Structure):
@@ -122,6 +123,19 @@ EXPORTS = {
     "mm_last_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
     "mm_set_profiling": (C.c_int, [P, C.c_int]),
     "mm_kernel_timing": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_int]),
+    # mm_comm.h
+    "mm_comm_unique_id": (C.c_int, [P, P]),
+    "mm_comm_init_rank": (C.c_int, [P, C.c_int, C.c_int, P, C.POINTER(P)]),
+    "mm_comm_init_all": (C.c_int, [C.c_int, P, P]),
+    "mm_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "mm_comm_rccl_version": (C.c_int, []),
+    "mm_comm_destroy": (None, [P]),
+    "mm_row_shard": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                               C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "mm_gather_rows": (C.c_int, [P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, C.c_uint32]),
+    "mm_gather_rows_all": (C.c_int, [C.c_int, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P,
+                                     C.c_uint32]),
+    "mm_assemble_rows": (C.c_int, [P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P]),
     # mm_scene.h
     "mm_rng_seed_from_u64": (None, [C.POINTER(mm_rng), C.c_uint64]),
     "mm_rng_from_seed": (None, [C.POINTER(mm_rng), P]),

@@ -65,3 +65,70 @@ def test_pmc_record_per_emulated_rank_share(monkeypatch):
     assert m["source"] is None and traffic is None
     m, _ = bench.pmc_profile(_args(), 20, 0.05, 8)  # N > 1 ranks: no single-GPU record applies
     assert m["source"] is None
+
+
+def _largs(gpus=1, launcher="auto"):
+    from types import SimpleNamespace
+
+    return SimpleNamespace(gpus=gpus, launcher=launcher)
+
+
+def test_gpus_n_without_a_launcher_starts_one_process_per_gpu():
+    """`bench.py --gpus 8` run on its own must run 8 GPUs,
+    not trace on one and print n_gpus 1.  Before torch or a GPU is touched it
+    starts torch.distributed.run with one process per GPU as a child (never
+    exec), with the same arguments; at N = 1 it runs in place unless
+    --launcher torchrun asks for the multi-GPU path at one rank."""
+    import bench
+
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    how, cmd = bench.launch_plan(_largs(8), {}, argv, port=29577)
+    assert how == "child"
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29577"
+    assert cmd[-len(argv) - 1:] == [str(bench.REPO / "bench.py")] + argv
+    assert bench.launch_plan(_largs(1), {}, ["--gpus", "1"]) == ("run", None)
+    how, cmd = bench.launch_plan(_largs(1, "torchrun"), {}, ["--gpus", "1", "--launcher", "torchrun"], port=1)
+    assert how == "child" and "--nproc-per-node=1" in cmd
+
+
+def test_gpus_must_match_the_launcher_world_size():
+    """Under a launcher (WORLD_SIZE set -- the driver's torchrun) the child
+    runs in place when WORLD_SIZE equals --gpus and refuses otherwise, so
+    n_gpus always equals --gpus."""
+    import bench
+
+    assert bench.launch_plan(_largs(8), {"WORLD_SIZE": "8"}, []) == ("run", None)
+    assert bench.launch_plan(_largs(1, "torchrun"), {"WORLD_SIZE": "1"}, []) == ("run", None)
+    how, msg = bench.launch_plan(_largs(8), {"WORLD_SIZE": "2"}, [])
+    assert how == "error" and "WORLD_SIZE=2" in msg and "--gpus 8" in msg
+    how, _ = bench.launch_plan(_largs(0), {}, [])
+    assert how == "error"
+
+
+def test_mismatch_exits_nonzero_before_touching_a_gpu():
+    """The refusal is an exit status, printed to stderr, with no JSON line."""
+    import os
+    import subprocess
+
+    import bench
+
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, str(bench.REPO / "bench.py"), "--gpus", "2"], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert p.returncode == 2 and p.stdout == "" and "WORLD_SIZE=4" in p.stderr
+
+
+def test_child_relay_passes_rank0_line_and_exit_status(tmp_path):
+    """relay_child: the child's JSON line is the one stdout line; other
+    stdout goes to stderr; a failing child's status is the parent's."""
+    import bench
+
+    script = tmp_path / "c.py"
+    script.write_text('import json,sys\nprint("banner")\nprint(json.dumps({"metric": "m", "value": 1}))\n'
+                      'sys.exit(int(sys.argv[1]))\n')
+    assert bench.relay_child([sys.executable, str(script), "0"]) == 0
+    assert bench.relay_child([sys.executable, str(script), "3"]) == 3
+    script.write_text("print('no line')\n")
+    assert bench.relay_child([sys.executable, str(script)]) == 1

@@ -221,3 +221,24 @@ def test_gloo_batch_gather_per_launch(world, sizes):
     for f in range(sum(sizes)):
         ref, _ = o.trace_tile(default_uniform(W, H, 0), make_ext(2, 3, 15, frame=f), 0, 0, W, H)
         assert frames[f].dtype == np.uint8 and np.array_equal(frames[f], quantize(ref)), f
+
+
+@pytest.mark.parametrize("height,world", [(1080, 8), (1080, 7), (2160, 3), (5, 8), (1, 1)])
+def test_row_shard_c_abi_matches_python(height, world):
+    """mm_row_shard (include/mm_comm.h, the split a Rust host would call) and
+    mirror_maze.dist.row_shard / rows_max name the same rows for every rank,
+    and the ranks' row sets partition the frame."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "mirror-maze_amd"))
+    from mirror_maze.comm import row_shard as c_shard
+    from mirror_maze.dist import row_shard, rows_max
+
+    seen = []
+    for rank in range(world):
+        y0, stride, rows, rm = c_shard(height, world, rank)
+        assert (y0, stride, rows) == row_shard(height, world, rank) and rm == rows_max(height, world)
+        seen += list(range(y0, height, stride))[:rows]
+        assert rows <= rm
+    assert sorted(seen) == list(range(height))

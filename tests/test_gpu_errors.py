@@ -369,3 +369,44 @@ def test_auto_tail_deferral_policy(gpu):
     assert r.scene_info(MM_INFO_LAST_DEFER) == 0.0 and r.scene_info(MM_INFO_LAST_LDS_MODE) == 14.0
     r.sync()
     r.close()
+
+
+def test_lost_ring_entry_ends_the_launch_quickly(gpu):
+    """after one protocol wait times out, the slot's turn word
+    never catches up, so every later wait of that slot would spin the whole
+    bound (2^20 polls, ~50 ms) and time out in turn -- a launch of minutes.
+    MM_OPT_FAULT_INJECT 4 loses the launch's first deferred path (its entry
+    is reserved and never written) with the NORMAL spin bound: its reader
+    times out once, every later wait sees the launch's error bit and gives
+    up within 256 polls, and the call fails by name, with the lost entry's
+    record, in well under a second of GPU time."""
+    import re
+    import time
+
+    import torch
+
+    from mirror_maze import MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    r.set_option(21, 64)  # every path defers at bounce 1: the rings cycle many laps
+    r.set_option(22, 0)
+    r.upload_scene(_scene(32))
+    u = default_uniform(512, 288, 0)
+    e = make_ext(8, 8, 8, frame=0)
+    r.set_option(23, 4)
+    t0 = time.time()
+    r.trace_tile(u, e, 0, 0, 512, 288)
+    call = r.last_call()
+    r.set_option(23, 0)
+    with pytest.raises(MMError) as ei:
+        r.sync()
+    dt = time.time() - t0
+    msg = str(ei.value)
+    assert f"call #{call} " in msg and "lost tail-ring entry" in msg, msg
+    assert "tail ring wait timed out" in msg and re.search(r"first timed-out wait \(launch \d+\): (reader|writer)", msg), msg
+    assert dt < 5.0, dt
+    # the record was consumed with its call; the context runs clean afterwards
+    again, _ = r.trace_tile(u, e, 0, 0, 512, 288)
+    r.sync()
+    assert torch.isfinite(again).all()
+    r.close()

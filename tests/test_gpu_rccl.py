@@ -1,7 +1,9 @@
-"""The multi-GPU frame path on the MI355X with the "nccl" backend (RCCL): a
-fresh torchrun process group renders frames through FrameGatherer
-(scripts/rccl_frames.py) and the assembled frames must equal trace_tile's,
-bit for bit.  The reference runs one Metal device (src/main.rs:616); the
+"""The multi-GPU frame path on the MI355X: a fresh torchrun job renders
+frames through the library's RCCL communicator (mm_comm_init_rank +
+mm_gather_rows, scripts/rccl_frames.py) and the assembled frames must equal
+trace_tile's, bit for bit; bench.py's N-GPU path, started by the driver's
+torchrun command and by `bench.py --gpus 1 --launcher torchrun`, delivers the
+same frame.  The reference runs one Metal device (src/main.rs:616); the
 gather is the build's replacement for that single-device plumbing."""
 from __future__ import annotations
 
@@ -50,14 +52,16 @@ def test_rccl_gathered_frames_equal_trace_tile(gpu, tmp_path, config, frames):
     r.close()
 
 
-@pytest.mark.parametrize("config", ["c2", "c3"])
-def test_bench_distributed_path_delivers_the_frame(gpu, tmp_path, config):
+@pytest.mark.parametrize("config,launcher", [("c2", "driver"), ("c3", "driver"), ("c2", "bench")])
+def test_bench_distributed_path_delivers_the_frame(gpu, tmp_path, config, launcher):
     """bench.py exactly as the driver launches it for N GPUs (torchrun, the
     "nccl" backend), at N = 1: batched launches, the RGBA8 conversion on the
     rank, the RCCL gather and the de-interleave on rank 0.  The frame rank 0
     holds after the timed steps must equal the texture-write conversion of
     trace_tile's last frame, byte for byte (C2: one launch without tail
-    deferral; C3: three frames, 50 M paths, with it)."""
+    deferral; C3: three frames, 50 M paths, with it).  launcher "bench":
+    `bench.py --gpus 1 --launcher torchrun` starts the same torchrun job as a
+    child and relays its line."""
     import json
 
     import torch
@@ -67,18 +71,24 @@ def test_bench_distributed_path_delivers_the_frame(gpu, tmp_path, config):
 
     out = tmp_path / "frame.npy"
     steps = 3
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"),
-           "--gpus", "1", "--config", config, "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline",
-           "--save-frame", str(out)]
+    args = ["--gpus", "1", "--config", config, "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline",
+            "--save-frame", str(out)]
+    if launcher == "driver":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py")] + args
+    else:
+        cmd = [sys.executable, str(REPO / "bench.py")] + args + ["--launcher", "torchrun"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
     assert p.returncode == 0, p.stderr[-3000:]
-    line = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][-1])
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["config"]["frame_format"] == "rgba8"
     assert "RCCL" in line["config"]["parallelism"]
     # the multi-GPU instrumentation, consistent at N = 1
     d = line["distributed"]
-    assert d["rccl_world"] == 1 and d["backend"] == "nccl"
+    assert d["rccl_world"] == 1 and d["torch_distributed_world"] == 1 and "mm_gather_rows" in d["backend"]
+    assert d["rccl_version"] >= 22600
     k = d["kernel_ms_per_rank"]
     assert k["min"] == k["max"] == k["rank0"] > 0
     assert abs(k["rank0"] - line["roofline"]["kernel_avg_ms"] * line["roofline"]["launches"]) < 0.01

@@ -23,7 +23,7 @@ def test_struct_sizes_match_reference_repr_c():
 
 def _declared_functions():
     names = set()
-    for h in ("mm_api.h", "mm_scene.h", "mm_io.h"):
+    for h in ("mm_api.h", "mm_scene.h", "mm_io.h", "mm_comm.h"):
         txt = (REPO / "include" / h).read_text()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         for m in re.finditer(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s+\**\s*(mm_[a-z_0-9]+)\s*\(", txt, flags=re.M):
