@@ -399,12 +399,15 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         }
         return true;
     };
-    // compact records: o_k, o_v, o_u (y first, above), class << 4 | axis << 20 | kind << 30 (the rect index,
-    // implied by the record's position, is dropped; the class's byte offset in the table is meta & 0x3F0,
-    // and a listed record's axis is x iff meta < 2^20); then the class table; then the leaf boxes
+    // compact records: the class table (kMaxClasses x 16 B), then per rect o_k, o_v, o_u (y first, above),
+    // class << 4 | axis << 20 | kind << 30 (the rect index, implied by the record's position, is dropped;
+    // the class's byte offset in the table is meta & 0x3F0, and a listed record's axis is x iff meta <
+    // 2^20); then the leaf boxes.  The table comes first so that, staged at LDS address 0, it and the
+    // records sit at compile-time offsets (mm_grid.h, trace_kernels.hip stage_and_run).
     auto compact_layout = [&](GridHost& gg) {
-        gg.off_class = align16(gg.off_recs + 16u * n_rects);
-        gg.off_box = align16(gg.off_class + 16u * kMaxClasses);
+        gg.off_class = gg.off_data = align16(gg.off_list + 2u * gg.n_list);
+        gg.off_recs = gg.off_class + kGridClassBytes;
+        gg.off_box = align16(gg.off_recs + 16u * n_rects);
         gg.bytes = align16(gg.off_box + 24u * n_rects);
     };
     double s = ext2[ext2.size() / 2] * cell_scale;
@@ -451,6 +454,7 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         std::memcpy(&g.image[g.off_class], cls.data(), 4 * cls.size());
     } else {
         g.off_class = 0;
+        g.off_data = g.off_recs;
         g.off_box = align16(g.off_recs + 32u * n_rects);
         g.bytes = align16(g.off_box + 24u * n_rects);
         g.image.resize(g.bytes);

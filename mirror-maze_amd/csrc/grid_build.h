@@ -12,6 +12,7 @@
 namespace mm {
 
 constexpr uint32_t kMaxClasses = 64;  // threshold classes of compact records (6 bits)
+constexpr uint32_t kGridClassBytes = 16 * kMaxClasses;  // the class table, ahead of the compact records
 
 struct GridHost {
     float mn[3], mx[3], cell[3], inv[3];
@@ -34,6 +35,10 @@ struct GridHost {
     bool slab = false;
     float slab_y[2] = {0.0f, 0.0f};
     uint32_t off_class = 0, n_class = 0;
+    // Where the data after the index (cells + lists) starts: the class table of compact records (which
+    // precedes their records, so a kernel that stages the data first finds the table at LDS address 0 and
+    // record k at kGridClassBytes + 16 k -- compile-time offsets), else the records.
+    uint32_t off_data = 0;
     std::vector<uint8_t> image;
 };
 

@@ -97,6 +97,7 @@ struct DevGrid {
     // each class (Yv_lo, Yv_hi, Yu_lo, Yu_hi) in a table after the records.
     const float4* cls;
     uint32_t off_class;        // 0: 32-B records (no class table)
+    uint32_t off_data;         // the data after the index: off_class (compact records), else off_recs
     // glob[0], glob[1] are y-normal FAST records in the planes y = slab_y[0] < slab_y[1] (grid_build.cpp)
     uint32_t slab;
     float slab_y[2];

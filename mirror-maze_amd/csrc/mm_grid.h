@@ -93,11 +93,35 @@ __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo
 __device__ __forceinline__ float sel_k(bool k0, bool k2, F3 v) { return k0 ? v.x : (k2 ? v.z : v.y); }
 __device__ __forceinline__ float sel_xy(bool sx, bool sy, F3 v) { return sx ? v.x : (sy ? v.y : v.z); }
 
+// A cell list's entries (u16 rect indices).  A walk keeps its list position
+// in the form the list's memory wants: in LDS the entry's byte address
+// (LdsList: base + 2 i, so a rect test loads its entry with no address
+// arithmetic -- ds_read_u16 straight from the position -- and steps by 2),
+// in global memory the entry index (GlobalList).
+struct LdsList {
+    uint32_t base;  // LDS byte address of entry 0
+    __device__ __forceinline__ uint32_t pos(uint32_t i) const { return base + 2u * i; }
+    static constexpr uint32_t kStep = 2;
+    __device__ __forceinline__ uint32_t at(uint32_t p) const {
+        return *(const __attribute__((address_space(3))) uint16_t*)(uintptr_t)p;
+    }
+};
+struct GlobalList {
+    const uint16_t* p;
+    __device__ __forceinline__ uint32_t pos(uint32_t i) const { return i; }
+    static constexpr uint32_t kStep = 1;
+    __device__ __forceinline__ uint32_t at(uint32_t i) const { return p[i]; }
+};
+// LDS byte address of an LDS object reached through a generic pointer.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;  // (an address-space cast)
+}
+
 // Where the grid's arrays are read from (LDS or global memory).
 template <typename CellsT, typename ListT, typename RecsT, typename BoxT, typename ClsT>
 struct GridView {
     CellsT cells;  // per cell: a 64-bit (wide) or 32-bit word (list range)
-    ListT list;    // rect indices (u16)
+    ListT list;    // rect indices (u16): LdsList or GlobalList
     RecsT recs;    // 2 x uint4 per rect, or 1 (compact records)
     BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
     ClsT cls;      // compact records' threshold classes (float4), else unused
@@ -339,8 +363,15 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             j1 = j0 + (cw >> 22);
         }
     };
+    // list positions (gv.list: entry byte addresses in LDS, indices in global memory)
     uint32_t j, jend;
-    cell_range(0u, j, jend);
+    auto cell_pos = [&](uint32_t sh) {
+        uint32_t j0, j1;
+        cell_range(sh, j0, j1);
+        j = gv.list.pos(j0);
+        jend = j + (j1 - j0) * gv.list.kStep;
+    };
+    cell_pos(0u);
     uint32_t cells = 1, tests = g.n_glob;
     // One iteration: test one rect of the current cell; when the cell's list
     // is done, step to the next cell (or stop) in the same iteration.
@@ -348,8 +379,8 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         MM_LANE_STAT(kLpGridIter);
         if (j < jend) {
             MM_LANE_STAT(kLpRectTest);
-            grid_rect<kSlow, kFlat, kFlat>(gv, geo, (uint32_t)gv.list[j], r, best, bk, tie);
-            ++j;
+            grid_rect<kSlow, kFlat, kFlat>(gv, geo, gv.list.at(j), r, best, bk, tie);
+            j += gv.list.kStep;
             if (kStats) ++tests;
         }
         if (j >= jend) {
@@ -376,7 +407,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             ty = sy ? nt : ty;
             tz = sz ? nt : tz;
             ci += sx ? dcx : (sy ? dcy : dcz);
-            cell_range((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu, j, jend);
+            cell_pos((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu);
             if (kStats) ++cells;
         }
     }

@@ -112,6 +112,9 @@ hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, floa
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s);
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
+// LDS modes 11 / 14 stage the grid image into a static array of this many bytes (ring: 0 none, 1 global
+// records, 2 records in LDS); other modes use dynamic LDS beside the kernel's static words.
+uint32_t wavepersist_grid_cap(int ring);
 // Whether the tail-deferral variant / any variant exists for this (LDS mode, form).
 bool wavepersist_defer_built(int lds_mode, int form);
 bool wavepersist_built(int lds_mode, int form);

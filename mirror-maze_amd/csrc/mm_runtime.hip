@@ -456,7 +456,7 @@ int mm_scene_info(const mm_ctx* c, int key, double* value) {
         case MM_INFO_GRID_CELLS_Z: *value = g.n[2]; return MM_OK;
         case MM_INFO_GRID_GLOBAL: *value = g.n_glob; return MM_OK;
         case MM_INFO_GRID_BYTES: *value = g.bytes; return MM_OK;
-        case MM_INFO_GRID_INDEX_BYTES: *value = g.off_recs; return MM_OK;
+        case MM_INFO_GRID_INDEX_BYTES: *value = g.off_data; return MM_OK;
         case MM_INFO_LEAN: *value = c->lean_ok ? 1.0 : 0.0; return MM_OK;
         case MM_INFO_DEPTH: *value = c->depth; return MM_OK;
         case MM_INFO_DICT_OK: *value = c->dict_ok ? 1.0 : 0.0; return MM_OK;
@@ -617,6 +617,7 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         dg.image = reinterpret_cast<const uint4*>(c->d_grid);
         dg.off_list = gh.off_list; dg.off_recs = gh.off_recs; dg.off_box = gh.off_box; dg.bytes = gh.bytes;
         dg.off_class = gh.off_class;  // 0: 32-byte records, no class table
+        dg.off_data = gh.off_data;
         dg.cls = gh.off_class ? reinterpret_cast<const float4*>(c->d_grid + gh.off_class) : nullptr;
         c->grid_slow = gh.n_slow > 0;
         c->grid_wide = gh.wide;
@@ -781,7 +782,7 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
         if (c->opt_lds && c->grid.bytes <= budget) return flat(11);
         // compact records + class table + index (N=64: ~77 KB), leaf boxes global
         if (c->opt_lds && c->grid_flat && c->grid.off_box <= budget) return flat(14);
-        if (c->opt_lds && c->grid.off_recs <= budget) return flat(12);
+        if (c->opt_lds && c->grid.off_data <= budget) return flat(12);
         if (!auto_form || !c->opt_lds) return flat(13);
         // the index does not fit LDS: auto takes the BVH (nodes in LDS or cached), which is not
         // measured against the all-global grid
@@ -890,10 +891,11 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     int ring = 0;
     if (defer) {
         const size_t img = wavepersist_lds_bytes(sc, mode);
+        const bool static_grid = mode == 11 || mode == 14;  // the image goes into the kernel's static array
         for (int kind : {2, 1}) {
             hipFuncAttributes dattr{};
             if (wavepersist_attributes(mode, form, kind, &dattr) == hipSuccess &&
-                img + dattr.sharedSizeBytes <= 80 * 1024) {
+                (static_grid ? img <= wavepersist_grid_cap(kind) : img + dattr.sharedSizeBytes <= 80 * 1024)) {
                 ring = kind;
                 break;
             }

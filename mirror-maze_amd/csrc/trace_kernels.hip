@@ -10,6 +10,7 @@
 //   k_resolve            per-pixel sample reduction in the reference's order
 #include <hip/hip_runtime.h>
 
+#include "grid_build.h"
 #include "mm_launch.h"
 #include "mm_path.h"
 #include "mm_wave_util.h"
@@ -690,7 +691,35 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
 //   14 grid records + class table + cells + lists, grid search (compact records: the maze forms)
 //      leaf boxes global
 // stage_and_run fills the block's LDS for the mode and calls body(query).
-template <int kLds, int kForm, bool kStats, typename F>
+//
+// Modes 11 and 14 stage the grid image into a STATIC LDS array (grid_lds):
+// its address is a compile-time constant, so the class table (LDS offset 0 of
+// the image) and record k (kGridClassBytes + 16 k) are read with the
+// constant folded into the ds_read instruction's immediate offset.  (The
+// base of the dynamic extern __shared__ array is a link-time relocation:
+// every address built on it costs a VALU add, and the three-operand
+// v_lshl_add_u32 and the SGPR-operand v_add_u32 it becomes cannot pair with
+// another wave's VALU op in a quad-cycle -- scripts/isa_dual.hip,
+// DESIGN.md s10.)  Each instance's array takes what the block's 80 KB leave
+// after its other static LDS (two 1024-thread blocks per CU).
+constexpr uint32_t kLdsPerBlock = 80 * 1024;
+template <int kRing>
+constexpr uint32_t grid_lds_cap() {
+    uint32_t other = kClaimWords * 16u * 4u + 64u;  // claimed queue ranges + alignment slack
+    if (kRing != 0) other += (4u + kTailRing) * 4u;  // ring counters and turn words
+    if (kRing == 2) other += 4u * kTailRing * 16u;   // ring payload
+#ifdef MM_LANE_STATS
+    other += 2u * kLpCount * 4u;
+#endif
+    return (kLdsPerBlock - other) & ~15u;
+}
+template <uint32_t kBytes>
+__device__ __forceinline__ uint4* grid_lds() {
+    __shared__ uint4 g[kBytes / 16u];
+    return g;
+}
+
+template <int kLds, int kForm, bool kStats, int kRing, typename F>
 __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const TileJob& job, F&& body) {
     extern __shared__ float4 lds[];
     auto staged = [&]() {  // diagnostics: time at which the block's LDS staging completed (wave timeline)
@@ -702,43 +731,44 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         }
     };
     if constexpr (kLds == 11 || kLds == 14) {
-        // records (+ class table) (+ boxes: mode 11) first, at LDS address 0 (a
-        // constant in the rect test), then cells + lists
-        const uint32_t end = kLds == 11 ? sc.grid.bytes : sc.grid.off_box;
-        const uint32_t nr16 = (end - sc.grid.off_recs) / 16u, ni16 = sc.grid.off_recs / 16u;
-        uint4* img = reinterpret_cast<uint4*>(lds);
+        // the data -- class table + records (+ boxes: mode 11) -- first, at the
+        // static array's start (compile-time offsets in the rect test), then
+        // cells + lists
+        const uint32_t d0 = sc.grid.off_data, end = kLds == 11 ? sc.grid.bytes : sc.grid.off_box;
+        const uint32_t nr16 = (end - d0) / 16u, ni16 = d0 / 16u;
+        uint4* img = grid_lds<grid_lds_cap<kRing>()>();
         const uint4* src = sc.grid.image;
         for (uint32_t i = threadIdx.x; i < nr16; i += blockDim.x) img[i] = src[ni16 + i];
         for (uint32_t i = threadIdx.x; i < ni16; i += blockDim.x) img[nr16 + i] = src[i];
         __syncthreads();
         staged();
-        const char* base = reinterpret_cast<const char*>(lds);
+        const char* base = reinterpret_cast<const char*>(img);
         const char* index = base + 16u * nr16;
-        const auto cls = reinterpret_cast<const float4*>(base + (sc.grid.off_class - sc.grid.off_recs));
+        // compact records: the class table at offset 0, record k at kGridClassBytes + 16 k; else records at 0
+        const auto recs = reinterpret_cast<const uint4*>(base + (grid_flat(kForm) ? kGridClassBytes : 0u));
+        const auto cls = reinterpret_cast<const float4*>(base);
         const auto run = [&](auto box) {
-            const auto gv = grid_view(reinterpret_cast<const char*>(index),
-                                      reinterpret_cast<const uint16_t*>(index + sc.grid.off_list),
-                                      reinterpret_cast<const uint4*>(lds), box, cls);
+            const auto gv = grid_view(reinterpret_cast<const char*>(index), LdsList{lds_addr(index + sc.grid.off_list)},
+                                      recs, box, cls);
             return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
         };
         if constexpr (kLds == 11)
-            return run(reinterpret_cast<const float2*>(base + (sc.grid.off_box - sc.grid.off_recs)));
+            return run(reinterpret_cast<const float2*>(base + (sc.grid.off_box - d0)));
         else
             return run(sc.grid.box);
     } else if constexpr (kLds == 12) {
-        const uint32_t n16 = sc.grid.off_recs / 16u;
+        const uint32_t n16 = sc.grid.off_data / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
         for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) img[i] = sc.grid.image[i];
         __syncthreads();
         staged();
         const char* base = reinterpret_cast<const char*>(lds);
-        const auto gv = grid_view(reinterpret_cast<const char*>(base),
-                                  reinterpret_cast<const uint16_t*>(base + sc.grid.off_list), sc.grid.recs,
-                                  sc.grid.box, sc.grid.cls);
+        const auto gv = grid_view(reinterpret_cast<const char*>(base), LdsList{lds_addr(base + sc.grid.off_list)},
+                                  sc.grid.recs, sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 13) {
-        const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), sc.grid.list, sc.grid.recs,
-                                  sc.grid.box, sc.grid.cls);
+        const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), GlobalList{sc.grid.list},
+                                  sc.grid.recs, sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 6) {
         for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
@@ -887,7 +917,7 @@ __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersis
 #else
     const unsigned long long t_entry = job.wave_ts ? (unsigned long long)wall_clock64() : 0ull;
 #endif
-    const uint32_t chunks = stage_and_run<kLds, kForm, kStats>(sc, job, [&](const auto& q) {
+    const uint32_t chunks = stage_and_run<kLds, kForm, kStats, kRing>(sc, job, [&](const auto& q) {
         if constexpr (kRing != 0)
             return wavepersist_ring_body<kStats, kRing == 2>(sc, q, job, samples, stats, err, work);
         else
@@ -902,10 +932,14 @@ __global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersis
     persistent_exit(job, chunks, t_entry, work, err);
 }
 
+uint32_t wavepersist_grid_cap(int ring) {
+    return ring == 2 ? grid_lds_cap<2>() : ring == 1 ? grid_lds_cap<1>() : grid_lds_cap<0>();
+}
+
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
     switch (lds_mode) {
         case 11: return sc.grid.bytes;
-        case 12: return sc.grid.off_recs;
+        case 12: return sc.grid.off_data;
         case 14: return sc.grid.off_box;
         case 6: return (size_t)sc.n_lds_f4 * sizeof(float4);
         case 10: return 256 * sizeof(float) + 3 * (size_t)sc.n_nodes * sizeof(uint32_t);
@@ -932,7 +966,11 @@ template <int kLds, int kForm, int kRing>
 static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        hipStream_t s) {
-    const size_t lds = wavepersist_lds_bytes(sc, kLds);  // (+ the tail ring's static LDS when kRing)
+    // modes 11 / 14 stage into the kernel's static grid array (stage_and_run): no dynamic LDS, and an image
+    // larger than the array is refused here (the host picks the ring kind so that it fits)
+    if ((kLds == 11 || kLds == 14) && wavepersist_lds_bytes(sc, kLds) > grid_lds_cap<kRing>())
+        return hipErrorInvalidValue;
+    const size_t lds = (kLds == 11 || kLds == 14) ? 0 : wavepersist_lds_bytes(sc, kLds);
     auto kern = count_stats ? k_trace_wavepersist<true, kLds, kForm, kRing>
                             : k_trace_wavepersist<false, kLds, kForm, kRing>;
     const uint32_t grid =

@@ -23,7 +23,7 @@ CLASSES = [
     ("waitcnt", re.compile(r"^s_waitcnt")),
     ("branch", re.compile(r"^s_(cbranch|branch|setpc|swappc|getpc)")),
     ("exec", re.compile(r"^s_\w+.*\bexec\b|^s_(and|or|andn2|xor)_saveexec")),
-    ("smem", re.compile(r"^s_(load|buffer_load|store|memtime|memrealtime|dcache)")),
+    ("smem", re.compile(r"^s_(load|buffer_load|memtime|memrealtime)")),
     ("sleep/nop", re.compile(r"^s_(sleep|nop|setprio|barrier|endpgm|trap)")),
     ("salu", re.compile(r"^s_")),
     ("readlane", re.compile(r"^v_(readfirstlane|readlane|writelane)")),

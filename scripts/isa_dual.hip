@@ -41,6 +41,18 @@ constexpr int kIters = 256;  // x 16 steps x 8 instructions per lane
 #define F_BFE(n) "v_bfe_u32 %" #n ", %" #n ", 3, 3\n\t"
 #define F_RCP(n) "v_rcp_f32 %" #n ", %" #n "\n\t"
 #define F_MULLO(n) "v_mul_lo_u32 %" #n ", %" #n ", %8\n\t"
+#define F_LSHL_K(n) "v_lshlrev_b32 %" #n ", 4, %" #n "\n\t"
+#define F_ADD_K(n) "v_add_u32 %" #n ", 2, %" #n "\n\t"
+#define F_AND_LIT(n) "v_and_b32 %" #n ", 0x3f0, %" #n "\n\t"
+#define F_MIN(n) "v_min_f32 %" #n ", %" #n ", %8\n\t"
+#define F_SUB(n) "v_sub_f32 %" #n ", %" #n ", %8\n\t"
+#define F_XOR(n) "v_xor_b32 %" #n ", %" #n ", %8\n\t"
+#define F_LSHR_V(n) "v_lshrrev_b32 %" #n ", %8, %" #n "\n\t"
+#define F_FMA_NEG(n) "v_fma_f32 %" #n ", -%" #n ", %8, %9\n\t"
+#define F_MUL_K(n) "v_mul_f32 %" #n ", 0x3dcccccd, %" #n "\n\t"
+#define F_ADDCO(n) "v_add_co_u32 %" #n ", vcc, %" #n ", %8\n\t"
+#define F_CNDV(n) "v_cmp_lt_f32 vcc, %" #n ", %8\n\tv_cndmask_b32 %" #n ", %" #n ", %9, vcc\n\t"
+#define F_MIX_SS(n) "v_cmp_lt_f32 vcc, %" #n ", %8\n\tv_cndmask_b32_e64 %" #n ", %" #n ", %9, %10\n\t"
 #define F_MIX(n) "v_fma_f32 %" #n ", %" #n ", %8, %9\n\tv_add_f32 %" #n ", %" #n ", %8\n\t"
 #define F_MIX_CMP(n) "v_cmp_lt_f32 vcc, %" #n ", %8\n\tv_add_f32 %" #n ", %" #n ", %8\n\t"
 
@@ -76,6 +88,18 @@ KERNEL(d_min3_f32, "", F_MIN3)
 KERNEL(d_bfe_u32, "", F_BFE)
 KERNEL(d_rcp_f32, "", F_RCP)
 KERNEL(d_mul_lo_u32, "", F_MULLO)
+KERNEL(d_lshl_k, "", F_LSHL_K)
+KERNEL(d_add_k, "", F_ADD_K)
+KERNEL(d_and_lit, "", F_AND_LIT)
+KERNEL(d_min_f32, "", F_MIN)
+KERNEL(d_sub_f32, "", F_SUB)
+KERNEL(d_xor_b32, "", F_XOR)
+KERNEL(d_lshr_v, "", F_LSHR_V)
+KERNEL(d_fma_neg, "", F_FMA_NEG)
+KERNEL(d_mul_lit, "", F_MUL_K)
+KERNEL(d_add_co, "", F_ADDCO)
+KERNEL(d_cmp_cnd, "", F_CNDV)
+KERNEL(d_mix_cmp_cnd64, "", F_MIX_SS)
 KERNEL(d_mix_fma_add, "", F_MIX)
 KERNEL(d_mix_cmp_add, "", F_MIX_CMP)
 
@@ -114,7 +138,13 @@ int main() {
         {"v_cmp_lt_f32 vcc", d_cmp_vcc, 1}, {"v_cmp_lt_f32_e64 s[]", d_cmp_e64, 1},
         {"v_readfirstlane_b32", d_readfirstlane, 1}, {"v_cvt_f32_i32", d_cvt_f32_i32, 1},
         {"v_min3_f32", d_min3_f32, 1}, {"v_bfe_u32", d_bfe_u32, 1}, {"v_rcp_f32", d_rcp_f32, 1},
-        {"v_mul_lo_u32", d_mul_lo_u32, 1}, {"fma + add", d_mix_fma_add, 2}, {"cmp vcc + add", d_mix_cmp_add, 2},
+        {"v_mul_lo_u32", d_mul_lo_u32, 1}, {"v_lshlrev_b32 inline k", d_lshl_k, 1},
+        {"v_add_u32 inline k", d_add_k, 1}, {"v_and_b32 literal", d_and_lit, 1}, {"v_min_f32", d_min_f32, 1},
+        {"v_sub_f32", d_sub_f32, 1}, {"v_xor_b32", d_xor_b32, 1}, {"v_lshrrev_b32 vgpr", d_lshr_v, 1},
+        {"v_fma_f32 neg src", d_fma_neg, 1}, {"v_mul_f32 literal", d_mul_lit, 1},
+        {"v_add_co_u32 (vcc out)", d_add_co, 1}, {"cmp vcc + cndmask vcc", d_cmp_cnd, 2},
+        {"cmp vcc + cndmask_e64", d_mix_cmp_cnd64, 2},
+        {"fma + add", d_mix_fma_add, 2}, {"cmp vcc + add", d_mix_cmp_add, 2},
     };
     printf("%d CUs, %d blocks x 256 threads (8 waves per SIMD), %d VALU per lane per kernel; clock attr %d MHz\n",
            cus, blocks, kIters * 16 * 8, clk_khz / 1000);
