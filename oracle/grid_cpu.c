@@ -48,6 +48,10 @@ typedef struct {
 } gridcpu_t;
 
 static gridcpu_t G;
+/* query counts since the last gridcpu_build: grid answers, walk fallbacks (ties, failed
+ * certificates, rays outside the guards / grid), and queries for a scene other than the one built -- those
+ * walk too, so a run that reports them is not the same-algorithm baseline */
+static uint64_t g_grid, g_fallback, g_other;
 
 static void rect_box(const mm_rect* r, double lo[3], double hi[3]) {
     for (int a = 0; a < 3; ++a) {
@@ -72,15 +76,46 @@ static void gridcpu_free(void) {
     memset(&G, 0, sizeof G);
 }
 
+/* The scene the grid was built for (NULL: none) -- one grid per process: a
+ * second build replaces the first, so callers check this before tracing. */
+const oracle_scene* gridcpu_scene(void) { return G.sc; }
+
+/* out[0] grid answers, out[1] walk fallbacks, out[2] queries for another scene (walked); reset = 1 zeroes. */
+void gridcpu_stats(uint64_t out[3], int reset) {
+    out[0] = __atomic_load_n(&g_grid, __ATOMIC_RELAXED);
+    out[1] = __atomic_load_n(&g_fallback, __ATOMIC_RELAXED);
+    out[2] = __atomic_load_n(&g_other, __ATOMIC_RELAXED);
+    if (reset) {
+        __atomic_store_n(&g_grid, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&g_fallback, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&g_other, 0, __ATOMIC_RELAXED);
+    }
+}
+
 /* Builds the grid for scene sc (kept for later oracle_trace_* calls of this
- * library); returns MM_OK or MM_ERR_NOMEM / MM_ERR_INVALID. */
+ * library); returns MM_OK or MM_ERR_NOMEM / MM_ERR_INVALID.  On failure no
+ * grid is left (gridcpu_scene() is NULL) and nothing leaks. */
+static int gridcpu_build_body(const oracle_scene* sc, uint32_t** cnt_p, uint8_t** is_glob_p);
 int gridcpu_build(const oracle_scene* sc) {
     gridcpu_free();
+    uint64_t junk[3];
+    gridcpu_stats(junk, 1);
+    uint32_t* cnt = NULL;
+    uint8_t* is_glob = NULL;
+    const int rc = gridcpu_build_body(sc, &cnt, &is_glob);
+    free(cnt);
+    free(is_glob);
+    if (rc != MM_OK) gridcpu_free();
+    return rc;
+}
+
+static int gridcpu_build_body(const oracle_scene* sc, uint32_t** cnt_p, uint8_t** is_glob_p) {
     const uint32_t nr = sc->n_rects;
     if (nr == 0) return MM_ERR_INVALID;
     G.sc = sc;
     double smin[3] = {1e30, 1e30, 1e30}, smax[3] = {-1e30, -1e30, -1e30}, C = 1.0;
     float* ext = malloc(4 * (size_t)nr);
+    if (!ext) return MM_ERR_NOMEM;
     uint32_t m = 0;
     for (uint32_t k = 0; k < nr; ++k) {
         double lo[3], hi[3], e1 = 0, e2 = 0;
@@ -112,8 +147,8 @@ int gridcpu_build(const oracle_scene* sc) {
         total *= n;
     }
     G.glob = malloc(4 * (size_t)nr);
-    uint32_t* cnt = calloc((size_t)total + 1, 4);
-    uint8_t* is_glob = calloc(nr, 1);
+    uint32_t* cnt = *cnt_p = calloc((size_t)total + 1, 4);
+    uint8_t* is_glob = *is_glob_p = calloc(nr, 1);
     if (!G.glob || !cnt || !is_glob) return MM_ERR_NOMEM;
     for (int pass = 0; pass < 2; ++pass) {
         for (uint32_t k = 0; k < nr; ++k) {
@@ -149,8 +184,6 @@ int gridcpu_build(const oracle_scene* sc) {
             memcpy(G.cell_off, cnt, 4 * ((size_t)total + 1));
         }
     }
-    free(cnt);
-    free(is_glob);
     G.leaf_of_rect = malloc(4 * (size_t)nr);
     G.n = malloc(sizeof(v3) * nr); G.o = malloc(sizeof(v3) * nr);
     G.v = malloc(sizeof(v3) * nr); G.u = malloc(sizeof(v3) * nr);
@@ -244,9 +277,14 @@ static int grid_search(const ray_t* b, float* t_out, uint32_t* i_out, uint64_t* 
 static void grid_query_or_walk(ray_t* b, const oracle_scene* sc, trav_t* tr) {
     float t;
     uint32_t k;
-    if (G.sc == sc && grid_search(b, &t, &k, &tr->rect_tests)) {
+    if (G.sc != sc) {
+        __atomic_fetch_add(&g_other, 1, __ATOMIC_RELAXED);
+    } else if (grid_search(b, &t, &k, &tr->rect_tests)) {
+        __atomic_fetch_add(&g_grid, 1, __ATOMIC_RELAXED);
         if (t < b->t) { b->t = t; b->index = k; }
         return;
+    } else {
+        __atomic_fetch_add(&g_fallback, 1, __ATOMIC_RELAXED);
     }
     intersect_bvh(b, sc, tr);
 }

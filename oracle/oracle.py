@@ -54,6 +54,10 @@ def grid_lib():
         L = _bind(GRID_LIB_PATH)
         L.gridcpu_build.argtypes = [C.c_void_p]
         L.gridcpu_build.restype = C.c_int
+        L.gridcpu_scene.argtypes = []
+        L.gridcpu_scene.restype = C.c_void_p
+        L.gridcpu_stats.argtypes = [C.c_void_p, C.c_int]
+        L.gridcpu_stats.restype = None
         _grid_lib = L
     return _grid_lib
 
@@ -116,10 +120,28 @@ class Oracle:
         if method == "grid":
             if grid_lib().gridcpu_build(C.byref(o.sc)) != 0:
                 raise RuntimeError("gridcpu_build failed")
-            o._lib = grid_lib
+            o._lib = o._grid_checked
         elif method != "walk":
             raise ValueError(method)
         return o
+
+    def _grid_checked(self):
+        """grid_lib(), after checking that the process's one grid is this
+        scene's: a later grid Oracle rebuilds it for its own scene, and this
+        one's queries would then silently walk the BVH."""
+        L = grid_lib()
+        if L.gridcpu_scene() != C.addressof(self.sc):
+            raise RuntimeError("grid_cpu holds another scene's grid (one grid per process): rebuild with "
+                               "Oracle.from_scene(s, method='grid')")
+        return L
+
+    @staticmethod
+    def grid_stats(reset: bool = False) -> dict:
+        """grid_cpu's query counts since the last build: grid answers, walk
+        fallbacks, and queries for another scene (walked)."""
+        out = (C.c_uint64 * 3)()
+        grid_lib().gridcpu_stats(out, 1 if reset else 0)
+        return {"grid": out[0], "fallback": out[1], "other_scene": out[2]}
 
     @staticmethod
     def _u(uniform) -> bytes:

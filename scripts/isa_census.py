@@ -42,6 +42,49 @@ def classify(ins: str) -> str:
     return "other"
 
 
+# Dual issue (scripts/isa_dual.hip, profiles/r05/isa_dual_r5c.txt): a SIMD-32 issues two wave64 VALU ops in a
+# quad-cycle only if at most one is "single-slot".  Pairable ("D") forms measured: v_add/sub/mul/fma/fmac_f32
+# (VGPR operands, literal or neg modifier allowed), v_add_u32 (VGPR or inline constant), v_and/v_xor (literal
+# allowed), v_lshrrev_b32 with a VGPR shift, v_mov_b32.  Single-slot ("S"): every form with an SGPR or VCC
+# operand (v_cmp*, v_cndmask*, readlane, carry-out adds), v_cvt*, three-source integer VOP3 (v_lshl_add,
+# v_bfe, v_min3), v_min/v_max, v_mul_lo, v_lshlrev_b32 with an inline constant, 64-bit ops; transcendentals
+# take two quads.
+D_FORMS = re.compile(r"^v_(add|sub|subrev|mul|fma|fmac)_f32|^v_(add|sub|subrev)_u32|^v_(and|or|xor)_b32|"
+                     r"^v_mov_b32|^v_lshrrev_b32|^v_ashrrev_i32")
+TRANS = re.compile(r"^v_(rcp|rsq|sqrt|exp|log|sin|cos)_")
+
+
+def slot(ins: str):
+    """'D', 'S' or 'T' (transcendental) for a VALU op, None otherwise."""
+    if not ins.startswith("v_"):
+        return None
+    if TRANS.search(ins):
+        return "T"
+    op, _, args = ins.partition(" ")
+    sgpr = re.search(r"\b(s\d+|s\[|vcc|exec|ttmp)", args)
+    if D_FORMS.search(op) and not sgpr and not op.endswith("_e64") or \
+            (D_FORMS.search(op) and op.endswith("_e64") and not sgpr and "v_add_co" not in op):
+        if op.startswith(("v_lshrrev_b32", "v_ashrrev_i32")) and re.match(r"\s*v\d+,\s*(-?\d+|0x)", args):
+            return "S"  # (a constant shift amount: measured single-slot for v_lshlrev_b32; assumed alike)
+        return "D"
+    return "S"
+
+
+def slots(items):
+    c = collections.Counter()
+    for kind, s in items:
+        if kind == "ins":
+            k = slot(s)
+            if k:
+                c[k] += 1
+    return c
+
+
+def quads(c):
+    """Idealised quad-cycles for a body's VALU ops: at most one single-slot op per quad, two ops per quad."""
+    return max(c["S"] + 2 * c["T"], (c["S"] + c["D"] + 2 * c["T"]) / 2)
+
+
 def kernel_lines(lines, key):
     """The kernel's body lines (label to .Lfunc_end) and its metadata .set lines."""
     start = None
@@ -121,6 +164,9 @@ def main():
     for s in spills:
         print("  " + s.lstrip("; "))
     print("whole kernel: " + fmt(census(items)))
+    sl = slots(items)
+    print(f"  VALU single-slot S={sl['S']} pairable D={sl['D']} transcendental T={sl['T']} "
+          f"(S share {sl['S'] / max(1, sum(sl.values())):.2f})")
     if a.loops:
         stack = []
         for lo, hi, t in loops(items):
@@ -128,7 +174,9 @@ def main():
                 stack.pop()
             c = census(items[lo:hi + 1])
             if sum(c.values()) >= a.min_body:
-                print(f"{'  ' * len(stack)}loop {t} (items {lo}-{hi}): " + fmt(c))
+                sl = slots(items[lo:hi + 1])
+                print(f"{'  ' * len(stack)}loop {t} (items {lo}-{hi}): " + fmt(c) +
+                      f" | VALU S={sl['S']} D={sl['D']} T={sl['T']} quads>={quads(sl):.1f}")
             stack.append((lo, hi))
 
 

@@ -30,7 +30,8 @@ for d in rows:
     sa = cb.get("same_algorithm") or {}
     same = f"{sa['value']} Mrays/s ({sa['cores']} cores)" if sa else "—"
     ref = r.get("reference_equivalent", r)  # (round-2 lines: the headline was the model)
-    hw = (f"{100 * r['frac']:.1f} % of {r['peak']} T" if r.get("basis", "").startswith("executed") else "—")
+    hw = (f"{100 * r['frac']:.1f} % of {r['peak']} T" if r.get("basis", "").startswith("executed") else
+          "— (PMC record of other sources)" if r.get("stale") else "—")
     print(f"| {c['workload']}{acc}{par} | {d['value']:.0f} Mrays/s | {d['ms_per_step']:.3f} | "
           f"{sc.get('value', '—')} Mrays/s | {cpu} | {same} | {hw} | {100 * ref['frac']:.1f} % of {r['peak']} T | "
           f"{100 * r['model_hbm']['frac']:.1f} % |")

@@ -132,3 +132,17 @@ def test_child_relay_passes_rank0_line_and_exit_status(tmp_path):
     assert bench.relay_child([sys.executable, str(script), "3"]) == 3
     script.write_text("print('no line')\n")
     assert bench.relay_child([sys.executable, str(script)]) == 1
+
+
+def test_stale_record_is_never_the_headline():
+    """with a PMC record of other sources the roofline headline
+    is the reference-walk model; the stale lane-ops rate sits only in the
+    labelled stale_profile sub-object and the line carries stale: true."""
+    import bench
+
+    measured = {"source": "profiles/pmc_c3.json", "stale": True, "stale_valu_lane_ops_tops": 30.0}
+    r = bench.roofline(40e12 * 0.05, 1e9, 0.05, 1, 20, measured, None, 1, {})
+    assert r["stale"] is True and r["achieved"] == 40.0 and r["basis"].startswith("reference_equivalent")
+    assert r["stale_profile"]["valu_lane_ops_tops"] == 30.0
+    fresh = bench.roofline(40e12 * 0.05, 1e9, 0.05, 1, 20, {"valu_lane_ops_tops": 29.0}, 5, 1, {})
+    assert fresh["stale"] is False and fresh["achieved"] == 29.0 and fresh["stale_profile"] is None

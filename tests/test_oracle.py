@@ -6,6 +6,7 @@ import ctypes as C
 import json
 
 import numpy as np
+import pytest
 
 from conftest import GOLDEN
 
@@ -176,3 +177,23 @@ def test_same_algorithm_cpu_baseline_equals_the_oracle():
         og.trace_group(u, chunks, gx, gy, fg)
     assert fw[..., 3].sum() == 4 * 16
     assert np.array_equal(fw.view(np.uint32), fg.view(np.uint32))
+
+
+def test_grid_baseline_refuses_another_scenes_grid():
+    """grid_cpu keeps one grid per process.  A second grid Oracle
+    rebuilds it for its scene; the first then refuses to trace (its queries
+    would otherwise walk the BVH under the same-algorithm label), and the
+    query counts separate grid answers from walk fallbacks."""
+    from mirror_maze import Scene, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    a = Oracle.from_scene(Scene.build(8, 0), method="grid")
+    u, e = default_uniform(64, 48, 0), make_ext(1, 2, 2)
+    a.trace_tile(u, e, 0, 0, 64, 48)
+    st = Oracle.grid_stats()
+    assert st["grid"] > 0 and st["other_scene"] == 0
+    b = Oracle.from_scene(Scene.build(9, 0), method="grid")
+    with pytest.raises(RuntimeError, match="another scene"):
+        a.trace_tile(u, e, 0, 0, 64, 48)
+    b.trace_tile(u, e, 0, 0, 64, 48)
+    assert Oracle.grid_stats()["other_scene"] == 0
