@@ -143,6 +143,12 @@ bool build_lists(const mm_rect* rects, uint32_t n_rects, const std::vector<uint3
         total *= g.n[a];
     }
     if (total > (1l << 20)) { why = "more than 2^20 cells"; return false; }
+    // the kernels' ray guard takes |o| <= 2^60 from the box (mm_trace.h ray_fast_ok_boxed)
+    for (int a = 0; a < 3; ++a)
+        if (!(std::fabs(g.mn[a]) <= 0x1p60f && std::fabs(g.mx[a]) <= 0x1p60f)) {
+            why = "grid box past 2^60";
+            return false;
+        }
     // cell ranges of every rect (widened by eps), global rects
     struct Span { int i0[3], i1[3]; long cover; };
     std::vector<Span> span(n_rects);
@@ -391,7 +397,8 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     // normal to x or z, and few distinct folded threshold tuples (C3: 22,
     // N=64: 26 -- the walls come in a handful of lengths and heights)
     auto maze_form = [&](const GridHost& gg) {
-        if (gg.n[1] != 1 || !classes_ok) return false;
+        // (the lists name rect k as 8 k in u16 entries: mm_grid.h rec_words)
+        if (gg.n[1] != 1 || !classes_ok || n_rects > 8191u) return false;
         for (uint32_t k = 0; k < n_rects; ++k) {
             const uint32_t meta = grecs[8 * (size_t)k + 7];
             const bool global = std::find(gg.glob, gg.glob + gg.n_glob, k) != gg.glob + gg.n_glob;
@@ -452,6 +459,13 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
             std::memcpy(&g.image[g.off_recs + 16u * k], r, 16);
         }
         std::memcpy(&g.image[g.off_class], cls.data(), 4 * cls.size());
+        // list entries name rect k as 8 k (record k's byte offset 16 k is then one pairable add)
+        for (uint32_t i = 0; i < g.n_list; ++i) {
+            uint16_t e;
+            std::memcpy(&e, &g.image[g.off_list + 2u * i], 2);
+            e = (uint16_t)(8u * e);
+            std::memcpy(&g.image[g.off_list + 2u * i], &e, 2);
+        }
     } else {
         g.off_class = 0;
         g.off_data = g.off_recs;

@@ -72,8 +72,9 @@ __device__ __forceinline__ void grid_update_sel(float a, uint32_t k, float& best
     best = lt ? a : best;
 }
 
-__device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo, uint32_t k, const Ray& r,
-                                                  float& best, uint32_t& bk, uint32_t& tie) {
+// (e: the rect's name in the search -- k, or 8 k in compact grids; rect_name)
+__device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo, uint32_t k, uint32_t e,
+                                                  const Ray& r, float& best, uint32_t& bk, uint32_t& tie) {
     const float4 g0 = geo[4 * k + 0], g1 = geo[4 * k + 1], g2 = geo[4 * k + 2], g3 = geo[4 * k + 3];
     const F3 o = xyz(g0), n = xyz(g1), v = xyz(g2), u = xyz(g3);
     const float lv = g0.w, lu = g1.w;
@@ -82,7 +83,7 @@ __device__ __forceinline__ void grid_rect_general(const float4* __restrict__ geo
     const F3 rv = (r.o - o) + a * r.d;
     const float d1 = qdiv(dot3(rv, v), lv, g2.w);
     const float d2 = qdiv(dot3(rv, u), lu, g3.w);
-    if (d1 >= 0.0f && d1 <= lv && d2 >= 0.0f && d2 <= lu && nc != 0.0f && a > 0.1f) grid_update(a, k, best, bk, tie);
+    if (d1 >= 0.0f && d1 <= lv && d2 >= 0.0f && d2 <= lu && nc != 0.0f && a > 0.1f) grid_update(a, e, best, bk, tie);
 }
 
 // Grid records (grid_build.cpp, 8 x u32 per rect, indexed by rect):
@@ -112,6 +113,33 @@ struct GlobalList {
     static constexpr uint32_t kStep = 1;
     __device__ __forceinline__ uint32_t at(uint32_t i) const { return p[i]; }
 };
+// The grid's cell words, read the same two ways: a walk in LDS keeps the
+// current cell as its word's LDS byte address (LdsCells: stepped by +-8 or +-4
+// times the cell-index step, so the read carries no address arithmetic and the
+// base is not reloaded per step), in global memory as the cell index.
+struct LdsCells {
+    uint32_t base;  // LDS byte address of cell 0's word
+    template <bool kWide>
+    static constexpr int kScale = kWide ? 8 : 4;
+    template <bool kWide>
+    __device__ __forceinline__ uint32_t pos(int ci) const { return base + (uint32_t)ci * (uint32_t)kScale<kWide>; }
+    __device__ __forceinline__ uint64_t at64(uint32_t p) const {
+        return *(const __attribute__((address_space(3))) uint64_t*)(uintptr_t)p;
+    }
+    __device__ __forceinline__ uint32_t at32(uint32_t p) const {
+        return *(const __attribute__((address_space(3))) uint32_t*)(uintptr_t)p;
+    }
+};
+struct GlobalCells {
+    const char* p;
+    template <bool kWide>
+    static constexpr int kScale = 1;
+    template <bool kWide>
+    __device__ __forceinline__ uint32_t pos(int ci) const { return (uint32_t)ci; }
+    __device__ __forceinline__ uint64_t at64(uint32_t i) const { return reinterpret_cast<const uint64_t*>(p)[i]; }
+    __device__ __forceinline__ uint32_t at32(uint32_t i) const { return reinterpret_cast<const uint32_t*>(p)[i]; }
+};
+
 // LDS byte address of an LDS object reached through a generic pointer.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;  // (an address-space cast)
@@ -120,7 +148,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // Where the grid's arrays are read from (LDS or global memory).
 template <typename CellsT, typename ListT, typename RecsT, typename BoxT, typename ClsT>
 struct GridView {
-    CellsT cells;  // per cell: a 64-bit (wide) or 32-bit word (list range)
+    CellsT cells;  // per cell: a 64-bit (wide) or 32-bit word (list range): LdsCells or GlobalCells
     ListT list;    // rect indices (u16): LdsList or GlobalList
     RecsT recs;    // 2 x uint4 per rect, or 1 (compact records)
     BoxT box;      // 3 x float2 per rect: its reference leaf's (mn, mx) per axis
@@ -136,10 +164,24 @@ __device__ __forceinline__ GridView<C, L, R, B, K> grid_view(C c, L l, R r, B b,
 // records hold both; compact records (kCompact, maze grids) hold w and their
 // class as class << 4 (meta bits 4-9, meta & 0x3F0 = the byte offset of the
 // class's 16-B entry in the class table; grid_build.cpp).
+// Compact (maze) grids name a rect as e = 8 k -- the list entries, the
+// global-rect indices, bk -- so that record k's byte offset 16 k = e + e is one
+// pairable v_add_u32 (a shift left is single-slot on gfx950, DESIGN.md §4;
+// written as asm because the compiler turns x + x into that shift).
+__device__ __forceinline__ uint32_t twice(uint32_t e) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(e));
+    return r;
+}
+template <bool kCompact>
+__device__ __forceinline__ constexpr uint32_t rect_name(uint32_t k) { return kCompact ? 8u * k : k; }
+template <bool kCompact>
+__device__ __forceinline__ constexpr uint32_t rect_index(uint32_t e) { return kCompact ? e >> 3 : e; }
+
 template <bool kCompact, typename GV>
 __device__ __forceinline__ uint4 rec_words(const GV& gv, uint32_t k) {
-    if constexpr (kCompact) {
-        return gv.recs[k];
+    if constexpr (kCompact) {  // k = e = 8 x the rect index (above)
+        return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(gv.recs) + twice(k));
     } else {
         const uint4 w0 = gv.recs[2 * k + 0];
         return make_uint4(w0.x, w0.y, w0.z, gv.recs[2 * k + 1].w);
@@ -166,7 +208,7 @@ __device__ __forceinline__ void grid_rect(const GV& gv, const float4* __restrict
     const uint32_t meta = w.w;
     if constexpr (kSlow) {
         if ((meta >> 30) == 2u) {
-            grid_rect_general(geo, k, r, best, bk, tie);
+            grid_rect_general(geo, rect_index<kCompact>(k), k, r, best, bk, tie);
             return;
         }
     }
@@ -223,7 +265,7 @@ __device__ __forceinline__ void grid_rect_uniform(const GV& gv, const float4* __
     const uint4 w = rec_words<kCompact>(gv, k);
     const uint32_t meta = __builtin_amdgcn_readfirstlane(w.w);
     if (kSlow && (meta >> 30) == 2u) {
-        grid_rect_general(geo, k, r, best, bk, tie);
+        grid_rect_general(geo, rect_index<kCompact>(k), k, r, best, bk, tie);
         return;
     }
     const uint32_t ak = (meta >> 20) & 3u;
@@ -288,7 +330,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         const bool lo_dead = r.d.y > 0.0f && g.slab_y[0] - r.o.y <= q;
         const bool hi_dead = r.d.y < 0.0f && g.slab_y[1] - r.o.y >= q;
         one = __builtin_amdgcn_ballot_w64(!(lo_dead || hi_dead)) == 0;
-        k1 = lo_dead ? g.glob[1] : g.glob[0];
+        k1 = rect_name<kFlat>(lo_dead ? g.glob[1] : g.glob[0]);
     }
     if (one) {
         MM_LANE_STAT(kLpGlobal);
@@ -296,7 +338,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     } else {
         for (uint32_t j = 0; j < g.n_glob; ++j) {
             MM_LANE_STAT(kLpGlobal);
-            grid_rect_uniform<kSlow, kFlat>(gv, geo, g.glob[j], r, best, bk, tie);
+            grid_rect_uniform<kSlow, kFlat>(gv, geo, rect_name<kFlat>(g.glob[j]), r, best, bk, tie);
         }
     }
     // The walk starts in the cell of the ray's point at t = 3/32, not at the
@@ -331,8 +373,8 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // across f did not already hold.  Plain (32-bit): first | count << 22.
     // face = 6: the whole list (the first cell).  (A run-time format flag
     // cost 2 % on C3: the format is a template parameter.)
-    // The current cell's index, stepped with the walk (+-1 per x step, +-n0 per
-    // z step (n0 n1 in 3-D), +-n0 per y step), and the bit offset of each
+    // The current cell, stepped with the walk (index +-1 per x step, +-n0 per
+    // z step (n0 n1 in 3-D), +-n0 per y step; as gv.cells' position), and the bit offset of each
     // axis's entry-face field in the wide cell word (25 + 6 f; the face
     // toward the previous cell is fixed per ray and axis), packed 8 bits per
     // axis: x, y, z.
@@ -342,23 +384,25 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         const int iy = kFlat ? 0 : (r.y.y > 0.0f ? by - 1 : by);
         ci = kFlat ? iz * g.n[0] + ix : (iz * g.n[1] + iy) * g.n[0] + ix;
     }
-    const int dcx = r.y.x > 0.0f ? 1 : -1;
-    const int dcz = (r.y.z > 0.0f ? 1 : -1) * (kFlat ? g.n[0] : g.n[0] * g.n[1]);
-    const int dcy = kFlat ? 0 : (r.y.y > 0.0f ? 1 : -1) * g.n[0];
+    // the walk's cell position (gv.cells: the word's LDS byte address, or the index) and its steps
+    constexpr int kCs = decltype(gv.cells)::template kScale<kWide>;
+    uint32_t cp = gv.cells.template pos<kWide>(ci);
+    const int dcx = r.y.x > 0.0f ? kCs : -kCs;
+    const int dcz = (r.y.z > 0.0f ? kCs : -kCs) * (kFlat ? g.n[0] : g.n[0] * g.n[1]);
+    const int dcy = kFlat ? 0 : (r.y.y > 0.0f ? kCs : -kCs) * g.n[0];
     const uint32_t fsh = (25u + (r.y.x > 0.0f ? 0u : 6u)) | ((37u + (r.y.y > 0.0f ? 0u : 6u)) << 8) |
                          ((49u + (r.y.z > 0.0f ? 0u : 6u)) << 16);
     // sh = 0: the whole list (the first cell)
     auto cell_range = [&](uint32_t sh, uint32_t& j0, uint32_t& j1) {
-        const uint32_t c = (uint32_t)ci;
         if constexpr (kWide) {
-            const uint64_t cw = reinterpret_cast<const uint64_t*>(gv.cells)[c];
+            const uint64_t cw = gv.cells.at64(cp);
             const bool whole = (cw >> 63) != 0;
             const uint32_t m = (uint32_t)(cw >> 22) & (whole ? 0x3FFu : 7u);
             const uint32_t fld = sh ? (uint32_t)(cw >> sh) & 63u : (m << 3);
             j0 = ((uint32_t)cw & 0x3FFFFFu) + (whole ? 0u : (fld & 7u));
             j1 = j0 + (whole ? m : (fld >> 3));
         } else {
-            const uint32_t cw = reinterpret_cast<const uint32_t*>(gv.cells)[c];
+            const uint32_t cw = gv.cells.at32(cp);
             j0 = cw & 0x3FFFFFu;
             j1 = j0 + (cw >> 22);
         }
@@ -373,17 +417,21 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     };
     cell_pos(0u);
     uint32_t cells = 1, tests = g.n_glob;
-    // One iteration: test one rect of the current cell; when the cell's list
-    // is done, step to the next cell (or stop) in the same iteration.
+    // Per cell: test the rects of its list, then step to the next cell (or
+    // stop).  (The compiler nests the tests in a per-cell loop either way;
+    // written as a do-while under one entry check, the loop carries one
+    // compare per test instead of a header and a latch compare.)
     for (;;) {
         MM_LANE_STAT(kLpGridIter);
         if (j < jend) {
-            MM_LANE_STAT(kLpRectTest);
-            grid_rect<kSlow, kFlat, kFlat>(gv, geo, gv.list.at(j), r, best, bk, tie);
-            j += gv.list.kStep;
-            if (kStats) ++tests;
+            do {
+                MM_LANE_STAT(kLpRectTest);
+                grid_rect<kSlow, kFlat, kFlat>(gv, geo, gv.list.at(j), r, best, bk, tie);
+                j += gv.list.kStep;
+                if (kStats) ++tests;
+            } while (j < jend);
         }
-        if (j >= jend) {
+        {
             MM_LANE_STAT(kLpCellStep);
             const float te = fminf(tx, fminf(ty, tz));
             if (best < te) break;
@@ -406,7 +454,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             tx = sx ? nt : tx;
             ty = sy ? nt : ty;
             tz = sz ? nt : tz;
-            ci += sx ? dcx : (sy ? dcy : dcz);
+            cp += (uint32_t)(sx ? dcx : (sy ? dcy : dcz));
             cell_pos((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu);
             if (kStats) ++cells;
         }
@@ -422,6 +470,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     if (tie) return false;
     MM_LANE_STAT(kLpCert);
     // certificate: R*'s reference leaf box passes at every t > best
+    bk = rect_index<kFlat>(bk);
     const float2 bxx = gv.box[3 * bk + 0], byy = gv.box[3 * bk + 1], bzz = gv.box[3 * bk + 2];
     const float tx1 = qdiv(bxx.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(bxx.y - r.o.x, r.d.x, r.y.x);
     float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);

@@ -38,8 +38,9 @@ struct GridQuery {
     __device__ __forceinline__ bool operator()(F3 o, F3 d, float& t, uint32_t& k, ScratchStack& st,
                                                Counters& c) const {
         const Ray r = make_ray(o, d);
-        bool guards = sc.fast_ok != 0;  // one branch for the three guards
-        guards &= ray_fast_ok(r);
+        // sc.fast_ok holds wherever a grid exists (mm_runtime.hip builds none
+        // otherwise), and the box check bounds |o| (ray_fast_ok_boxed)
+        bool guards = ray_fast_ok_boxed(r);  // one branch for the guards
         guards &= grid_ray_ok(sc.grid, r);
         if (guards && grid_search<kStats, kSlow, kWide, kFlat>(sc.grid, gv, sc.geo, r, t, k, c)) return true;
         MM_LANE_STAT(kLpFallback);

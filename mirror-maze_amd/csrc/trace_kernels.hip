@@ -748,7 +748,7 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         const auto recs = reinterpret_cast<const uint4*>(base + (grid_flat(kForm) ? kGridClassBytes : 0u));
         const auto cls = reinterpret_cast<const float4*>(base);
         const auto run = [&](auto box) {
-            const auto gv = grid_view(reinterpret_cast<const char*>(index), LdsList{lds_addr(index + sc.grid.off_list)},
+            const auto gv = grid_view(LdsCells{lds_addr(index)}, LdsList{lds_addr(index + sc.grid.off_list)},
                                       recs, box, cls);
             return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
         };
@@ -763,11 +763,11 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         __syncthreads();
         staged();
         const char* base = reinterpret_cast<const char*>(lds);
-        const auto gv = grid_view(reinterpret_cast<const char*>(base), LdsList{lds_addr(base + sc.grid.off_list)},
+        const auto gv = grid_view(LdsCells{lds_addr(base)}, LdsList{lds_addr(base + sc.grid.off_list)},
                                   sc.grid.recs, sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 13) {
-        const auto gv = grid_view(reinterpret_cast<const char*>(sc.grid.cells), GlobalList{sc.grid.list},
+        const auto gv = grid_view(GlobalCells{reinterpret_cast<const char*>(sc.grid.cells)}, GlobalList{sc.grid.list},
                                   sc.grid.recs, sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
     } else if constexpr (kLds == 6) {

@@ -44,11 +44,12 @@ def classify(ins: str) -> str:
 
 # Dual issue (scripts/isa_dual.hip, profiles/r05/isa_dual_r5c.txt): a SIMD-32 issues two wave64 VALU ops in a
 # quad-cycle only if at most one is "single-slot".  Pairable ("D") forms measured: v_add/sub/mul/fma/fmac_f32
-# (VGPR operands, literal or neg modifier allowed), v_add_u32 (VGPR or inline constant), v_and/v_xor (literal
-# allowed), v_lshrrev_b32 with a VGPR shift, v_mov_b32.  Single-slot ("S"): every form with an SGPR or VCC
-# operand (v_cmp*, v_cndmask*, readlane, carry-out adds), v_cvt*, three-source integer VOP3 (v_lshl_add,
-# v_bfe, v_min3), v_min/v_max, v_mul_lo, v_lshlrev_b32 with an inline constant, 64-bit ops; transcendentals
-# take two quads.
+# (VGPR operands, literal or neg modifier allowed), v_add_u32 (VGPR, inline constant or literal; x + x),
+# v_and/v_or/v_xor (literal allowed), v_lshrrev_b32 (by a VGPR or a constant), v_mov_b32.  Single-slot
+# ("S"): every form with an SGPR or VCC operand (v_cmp*, v_cndmask*, readlane, carry-out adds), v_cvt*,
+# three-source VOP3 (v_lshl_add, v_bfe, v_min3, v_max3_u32, v_or3), v_min/v_max, v_mul_lo, v_mul_u32_u24,
+# v_lshlrev_b32 (by a constant or a VGPR), 64-bit ops; transcendentals take two quads
+# (profiles/r05/isa_dual_r5c.txt, isa_dual_r5g.txt).
 D_FORMS = re.compile(r"^v_(add|sub|subrev|mul|fma|fmac)_f32|^v_(add|sub|subrev)_u32|^v_(and|or|xor)_b32|"
                      r"^v_mov_b32|^v_lshrrev_b32|^v_ashrrev_i32")
 TRANS = re.compile(r"^v_(rcp|rsq|sqrt|exp|log|sin|cos)_")

@@ -48,6 +48,14 @@ constexpr int kIters = 256;  // x 16 steps x 8 instructions per lane
 #define F_SUB(n) "v_sub_f32 %" #n ", %" #n ", %8\n\t"
 #define F_XOR(n) "v_xor_b32 %" #n ", %" #n ", %8\n\t"
 #define F_LSHR_V(n) "v_lshrrev_b32 %" #n ", %8, %" #n "\n\t"
+#define F_LSHL_V(n) "v_lshlrev_b32 %" #n ", %8, %" #n "\n\t"
+#define F_LSHR_K(n) "v_lshrrev_b32 %" #n ", 4, %" #n "\n\t"
+#define F_ADDU_LIT(n) "v_add_u32 %" #n ", 0xd4800000, %" #n "\n\t"
+#define F_ADDU_SELF(n) "v_add_u32 %" #n ", %" #n ", %" #n "\n\t"
+#define F_MAX3U(n) "v_max3_u32 %" #n ", %" #n ", %8, %9\n\t"
+#define F_OR3(n) "v_or3_b32 %" #n ", %" #n ", %8, %9\n\t"
+#define F_OR(n) "v_or_b32 %" #n ", %" #n ", %8\n\t"
+#define F_MULU24(n) "v_mul_u32_u24 %" #n ", %" #n ", %8\n\t"
 #define F_FMA_NEG(n) "v_fma_f32 %" #n ", -%" #n ", %8, %9\n\t"
 #define F_MUL_K(n) "v_mul_f32 %" #n ", 0x3dcccccd, %" #n "\n\t"
 #define F_ADDCO(n) "v_add_co_u32 %" #n ", vcc, %" #n ", %8\n\t"
@@ -96,6 +104,14 @@ KERNEL(d_sub_f32, "", F_SUB)
 KERNEL(d_xor_b32, "", F_XOR)
 KERNEL(d_lshr_v, "", F_LSHR_V)
 KERNEL(d_fma_neg, "", F_FMA_NEG)
+KERNEL(d_lshl_v, "", F_LSHL_V)
+KERNEL(d_lshr_k, "", F_LSHR_K)
+KERNEL(d_addu_lit, "", F_ADDU_LIT)
+KERNEL(d_addu_self, "", F_ADDU_SELF)
+KERNEL(d_max3_u32, "", F_MAX3U)
+KERNEL(d_or3_b32, "", F_OR3)
+KERNEL(d_or_b32, "", F_OR)
+KERNEL(d_mul_u24, "", F_MULU24)
 KERNEL(d_mul_lit, "", F_MUL_K)
 KERNEL(d_add_co, "", F_ADDCO)
 KERNEL(d_cmp_cnd, "", F_CNDV)
@@ -145,6 +161,9 @@ int main() {
         {"v_add_co_u32 (vcc out)", d_add_co, 1}, {"cmp vcc + cndmask vcc", d_cmp_cnd, 2},
         {"cmp vcc + cndmask_e64", d_mix_cmp_cnd64, 2},
         {"fma + add", d_mix_fma_add, 2}, {"cmp vcc + add", d_mix_cmp_add, 2},
+        {"v_lshlrev_b32 vgpr", d_lshl_v, 1}, {"v_lshrrev_b32 inline k", d_lshr_k, 1},
+        {"v_add_u32 literal", d_addu_lit, 1}, {"v_add_u32 x + x", d_addu_self, 1}, {"v_max3_u32", d_max3_u32, 1},
+        {"v_or3_b32", d_or3_b32, 1}, {"v_or_b32", d_or_b32, 1}, {"v_mul_u32_u24", d_mul_u24, 1},
     };
     printf("%d CUs, %d blocks x 256 threads (8 waves per SIMD), %d VALU per lane per kernel; clock attr %d MHz\n",
            cus, blocks, kIters * 16 * 8, clk_khz / 1000);
