@@ -140,6 +140,22 @@ struct GlobalCells {
     __device__ __forceinline__ uint32_t at32(uint32_t i) const { return reinterpret_cast<const uint32_t*>(p)[i]; }
 };
 
+// Cell words staged into LDS (trace_kernels.hip stage_and_run): the
+// first-entry field (bits 0-21) becomes the LDS byte address of that entry,
+// lbase + 2 first (< 2^22), so the walk reads list ranges without address
+// arithmetic (grid_search, cell_pos).  v: 16 bytes of the cells section.
+template <bool kWide>
+__device__ __forceinline__ uint4 grid_stage_cells(uint4 v, uint32_t lbase) {
+    auto fix = [&](uint32_t w) { return (w & ~0x3FFFFFu) | (lbase + 2u * (w & 0x3FFFFFu)); };
+    v.x = fix(v.x);
+    v.z = fix(v.z);
+    if (!kWide) {
+        v.y = fix(v.y);
+        v.w = fix(v.w);
+    }
+    return v;
+}
+
 // LDS byte address of an LDS object reached through a generic pointer.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;  // (an address-space cast)
@@ -393,27 +409,34 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     const uint32_t fsh = (25u + (r.y.x > 0.0f ? 0u : 6u)) | ((37u + (r.y.y > 0.0f ? 0u : 6u)) << 8) |
                          ((49u + (r.y.z > 0.0f ? 0u : 6u)) << 16);
     // sh = 0: the whole list (the first cell)
-    auto cell_range = [&](uint32_t sh, uint32_t& j0, uint32_t& j1) {
-        if constexpr (kWide) {
-            const uint64_t cw = gv.cells.at64(cp);
-            const bool whole = (cw >> 63) != 0;
-            const uint32_t m = (uint32_t)(cw >> 22) & (whole ? 0x3FFu : 7u);
-            const uint32_t fld = sh ? (uint32_t)(cw >> sh) & 63u : (m << 3);
-            j0 = ((uint32_t)cw & 0x3FFFFFu) + (whole ? 0u : (fld & 7u));
-            j1 = j0 + (whole ? m : (fld >> 3));
-        } else {
-            const uint32_t cw = gv.cells.at32(cp);
-            j0 = cw & 0x3FFFFFu;
-            j1 = j0 + (cw >> 22);
-        }
-    };
-    // list positions (gv.list: entry byte addresses in LDS, indices in global memory)
+    // The cell's list range [j, jend) in gv.list's positions: in LDS entry
+    // byte addresses -- the staged cell words' first-entry fields already hold
+    // them (grid_stage_cells), so the decode doubles the counts, and does it
+    // without a shift left (single-slot on gfx950) --, in global
+    // memory entry indices.
     uint32_t j, jend;
     auto cell_pos = [&](uint32_t sh) {
-        uint32_t j0, j1;
-        cell_range(sh, j0, j1);
-        j = gv.list.pos(j0);
-        jend = j + (j1 - j0) * gv.list.kStep;
+        constexpr bool kB = decltype(gv.list)::kStep == 2u;
+        if constexpr (kWide) {
+            const uint64_t cw = gv.cells.at64(cp);
+            const uint32_t lo = (uint32_t)cw;
+            const bool whole = (int32_t)(uint32_t)(cw >> 32) < 0;
+            const uint32_t first = lo & 0x3FFFFFu;
+            const uint32_t m = kB ? (lo >> 21) & (whole ? 0x7FEu : 0xEu) : (lo >> 22) & (whole ? 0x3FFu : 7u);
+            if (sh == 0u) {  // the whole list (the first cell)
+                j = first;
+                jend = first + m;
+            } else {
+                const uint32_t f = (uint32_t)(cw >> sh);
+                const uint32_t st = kB ? (twice(f) & 14u) : (f & 7u), len = kB ? ((f >> 2) & 14u) : ((f >> 3) & 7u);
+                j = first + (whole ? 0u : st);
+                jend = j + (whole ? m : len);
+            }
+        } else {
+            const uint32_t cw = gv.cells.at32(cp);
+            j = cw & 0x3FFFFFu;
+            jend = j + (kB ? ((cw >> 21) & 0x7FEu) : (cw >> 22));
+        }
     };
     cell_pos(0u);
     uint32_t cells = 1, tests = g.n_glob;

@@ -739,7 +739,11 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         uint4* img = grid_lds<grid_lds_cap<kRing>()>();
         const uint4* src = sc.grid.image;
         for (uint32_t i = threadIdx.x; i < nr16; i += blockDim.x) img[i] = src[ni16 + i];
-        for (uint32_t i = threadIdx.x; i < ni16; i += blockDim.x) img[nr16 + i] = src[i];
+        {  // cells (their first-entry fields as LDS byte addresses: grid_stage_cells), then lists
+            const uint32_t nc16 = sc.grid.off_list / 16u, lbase = lds_addr(img + nr16) + sc.grid.off_list;
+            for (uint32_t i = threadIdx.x; i < ni16; i += blockDim.x)
+                img[nr16 + i] = i < nc16 ? grid_stage_cells<grid_wide(kForm)>(src[i], lbase) : src[i];
+        }
         __syncthreads();
         staged();
         const char* base = reinterpret_cast<const char*>(img);
@@ -757,9 +761,11 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         else
             return run(sc.grid.box);
     } else if constexpr (kLds == 12) {
-        const uint32_t n16 = sc.grid.off_data / 16u;
+        const uint32_t n16 = sc.grid.off_data / 16u, nc16 = sc.grid.off_list / 16u;
         uint4* img = reinterpret_cast<uint4*>(lds);
-        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) img[i] = sc.grid.image[i];
+        const uint32_t lbase = lds_addr(img) + sc.grid.off_list;
+        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x)
+            img[i] = i < nc16 ? grid_stage_cells<grid_wide(kForm)>(sc.grid.image[i], lbase) : sc.grid.image[i];
         __syncthreads();
         staged();
         const char* base = reinterpret_cast<const char*>(lds);

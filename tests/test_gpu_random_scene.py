@@ -99,3 +99,31 @@ def test_random_scene_windows_bit_exact(gpu, lattice, case):
     assert r.scene_info(MM_INFO_LAST_FORM) == expect[0]
     assert r.scene_info(MM_INFO_LAST_LDS_MODE) in expect[1]
     r.close()
+
+
+def test_scene_reaching_2_60_takes_the_bvh_bit_exact(gpu):
+    """A rect corner at x = 2^60: the scene is inside the exact-division
+    guards (every coordinate <= 2^60), but its grid box (widened by eps) would
+    pass 2^60, which the per-query guard's integer form takes from the box
+    (mm_trace.h ray_fast_ok_boxed) -- grid_build.cpp builds no grid, the
+    queries walk the BVH, and the frames stay bit-exact."""
+    from mirror_maze import MM_INFO_GRID_OK, Renderer, Scene, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = random_scene(300, 5, False)
+    rects = s.rects.copy()
+    rects[0, 0:9] = np.float32([2.0**60 - 2.0**58, -8.0, 0.0, 2.0**58, 0.0, 0.0, 0.0, 16.0, 0.0])
+    nodes, idx = Scene.bvh(rects)
+    s = Scene(0, rects, nodes, idx, s.is_mirror, s.emission, np.zeros((0, 0), np.uint8), 0)
+    o = Oracle.from_scene(s)
+    r = Renderer(0)
+    r.upload_scene(s)
+    assert r.scene_info(MM_INFO_GRID_OK) == 0.0
+    u = default_uniform(1920, 1080, 0)
+    e = make_ext(8, 8, 8, frame=3)
+    for (x0, y0) in [(0, 0), (944, 532), (1500, 200)]:
+        got, st = r.trace_tile(u, e, x0, y0, 32, 16, stats=True)
+        ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
+        assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
+        assert (st.rays, st.paths) == (rst.rays, rst.paths)
+    r.close()
