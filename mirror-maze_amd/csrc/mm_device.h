@@ -101,6 +101,10 @@ struct DevGrid {
     // glob[0], glob[1] are y-normal FAST records in the planes y = slab_y[0] < slab_y[1] (grid_build.cpp)
     uint32_t slab;
     float slab_y[2];
+    // n[a] - 1, a kernel argument of its own: the kernel reloads it where the
+    // walk clamps a cell index instead of keeping a computed n - 1 live (the
+    // compiler spills those to VGPR lanes: a single-slot v_readlane per use)
+    int nm1[3];
 };
 
 struct DevScene {

@@ -303,7 +303,18 @@ __device__ __forceinline__ bool grid_ray_ok(const DevGrid& g, const Ray& r) {
 
 __device__ __forceinline__ int grid_cell(const DevGrid& g, float o, int a) {
     const int i = (int)floorf((o - g.mn[a]) * g.inv[a]);
-    return min(max(i, 0), g.n[a] - 1);
+    return min(max(i, 0), g.nm1[a]);
+}
+
+// A kernel-argument value read at its use.  A uniform branch on a kernel
+// argument inside the walk is otherwise hoisted out of the bounce loop as a
+// 64-bit lane mask, which the compiler then spills to VGPR lanes (two
+// single-slot v_readlane per use); through the asm the compare
+// stays at the branch and the argument is reloaded (s_load) when needed.
+__device__ __forceinline__ uint32_t arg_at_use(uint32_t v) {
+    uint32_t r;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+    return r;
 }
 
 // DDA state per axis: the index b of the next cell boundary the ray crosses
@@ -315,7 +326,7 @@ __device__ __forceinline__ float grid_time(const DevGrid& g, int a, int b, float
     return ((g.mn[a] + (float)b * g.cell[a]) - o) * y;
 }
 __device__ __forceinline__ int grid_first(const DevGrid& g, int a, float o, float y) {
-    const int i = min(max((int)floorf((o - g.mn[a]) * g.inv[a]), 0), g.n[a] - 1);
+    const int i = min(max((int)floorf((o - g.mn[a]) * g.inv[a]), 0), g.nm1[a]);
     return y > 0.0f ? i + 1 : i;
 }
 
@@ -341,7 +352,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     // two, each lane tests only the other (its record read per lane).
     bool one = false;
     uint32_t k1 = 0;
-    if (g.slab) {
+    if (arg_at_use(g.slab)) {
         const float q = 0.05f * r.d.y;
         const bool lo_dead = r.d.y > 0.0f && g.slab_y[0] - r.o.y <= q;
         const bool hi_dead = r.d.y < 0.0f && g.slab_y[1] - r.o.y >= q;
@@ -352,7 +363,7 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         MM_LANE_STAT(kLpGlobal);
         grid_rect_axis<1, kFlat>(gv, k1, rec_words<kFlat>(gv, k1), r, best, bk, tie);
     } else {
-        for (uint32_t j = 0; j < g.n_glob; ++j) {
+        for (uint32_t j = 0, n = arg_at_use(g.n_glob); j < n; ++j) {
             MM_LANE_STAT(kLpGlobal);
             grid_rect_uniform<kSlow, kFlat>(gv, geo, rect_name<kFlat>(g.glob[j]), r, best, bk, tie);
         }
@@ -466,7 +477,8 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
             bx += sx ? (r.y.x > 0.0f ? 1 : -1) : 0;
             by += sy ? (r.y.y > 0.0f ? 1 : -1) : 0;
             bz += sz ? (r.y.z > 0.0f ? 1 : -1) : 0;
-            if (((uint32_t)bx > (uint32_t)g.n[0]) | ((uint32_t)by > (uint32_t)g.n[1]) |
+            // (kFlat: by never moves from 0 / 1 and n[1] == 1)
+            if (((uint32_t)bx > (uint32_t)g.n[0]) | (!kFlat && (uint32_t)by > (uint32_t)g.n[1]) |
                 ((uint32_t)bz > (uint32_t)g.n[2]))
                 break;
             // grid_time of the stepped axis, the same operations on selected operands
