@@ -197,3 +197,34 @@ def test_grid_baseline_refuses_another_scenes_grid():
         a.trace_tile(u, e, 0, 0, 64, 48)
     b.trace_tile(u, e, 0, 0, 64, 48)
     assert Oracle.grid_stats()["other_scene"] == 0
+
+
+def test_grid_baseline_counts_every_query_across_threads():
+    """The same-algorithm baseline's query counters are per thread (one shared
+    atomic made the 16-thread baseline 12x slower in round 5): traced from
+    four threads at once, the grid answers plus walk fallbacks still equal the
+    rays the rows report, and a reset zeroes every thread's slot."""
+    import threading
+
+    from mirror_maze import Scene, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    o = Oracle.from_scene(Scene.build(16, 0), method="grid")
+    u, e = default_uniform(256, 64, 0), make_ext(2, 4, 4, frame=1)
+    Oracle.grid_stats(reset=True)
+    rays = [0] * 4
+
+    def work(i):
+        for y in range(i, 64, 4):
+            _, st = o.trace_tile(u, e, 0, y, 256, 1)
+            rays[i] += st.rays
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    st = Oracle.grid_stats(reset=True)
+    assert st["other_scene"] == 0
+    assert st["grid"] + st["fallback"] == sum(rays) > 0
+    assert Oracle.grid_stats() == {"grid": 0, "fallback": 0, "other_scene": 0}
