@@ -109,7 +109,7 @@ def parse():
     p.add_argument("--frame-format", default="rgba8", choices=["rgba8", "f32"],
                    help="format of the frame each step delivers on rank 0: rgba8 = the reference's output "
                         "texture format (RGBA8Unorm, src/main.rs:702-709; the texture-write conversion "
-                        "mm_quantize_rgba8 on each rank, then the gather moves 4 B/px), f32 = the float tile "
+                        "written by the trace itself, MM_EXT_RGBA8, then the gather moves 4 B/px), f32 = the float tile "
                         "(16 B/px).  Accumulated runs (--accumulate) gather their f32 running sum.")
     p.add_argument("--accumulate", action="store_true",
                    help="temporal accumulation (C5): every frame adds into one running sum per rank "
@@ -452,16 +452,14 @@ def main():
                 if distributed else None)
     bgather = gatherer if distributed and fb_max > 1 else None
     tiles1 = None if distributed else [torch.zeros((H, W, 4), dtype=fdt, device=dev) for _ in rens]
-    # float tiles the trace writes when the delivered frame is RGBA8 (one per context)
-    ftiles = [torch.zeros((rows_max(H, world), W, 4), dtype=torch.float32, device=dev) for _ in rens] if rgba8 else None
     last = [0]
     active = [len(rens)]  # contexts the frames alternate over
     batch = [1]           # frames per launch (mm_trace_tile_frames), single context
     # per context: the launch's float frames (and their RGBA8 conversions on one GPU)
-    batch_bufs = [torch.zeros((fb_max, my_rows, W, 4), dtype=torch.float32, device=dev) if fb_max > 1 else None
-                  for _ in rens]
+    batch_bufs = [torch.zeros((fb_max, my_rows, W, 4), dtype=torch.float32, device=dev)
+                  if fb_max > 1 and not rgba8 else None for _ in rens]
     batch_bufs8 = [torch.zeros((fb_max, my_rows, W, 4), dtype=torch.uint8, device=dev)
-                   if fb_max > 1 and rgba8 and not distributed else None for _ in rens]
+                   if fb_max > 1 and rgba8 else None for _ in rens]
     progress_t = [time.perf_counter()]
 
     def progress(msg):
@@ -486,13 +484,11 @@ def main():
                     trace_end[0].record(streams[slot])
                 return st
             tile = gatherer.tiles(1)[0] if gatherer else tiles1[slot]
-            ft = ftiles[slot] if rgba8 else tile
+            # (an RGBA8 tile: the library writes the texture-write conversion itself, MM_EXT_RGBA8)
             _, st = rens[slot].trace_tile(u, make_ext(spp, bl, ml, frame=frame), 0, y0, W, my_rows,
-                                          y_stride=y_stride, out=ft[:my_rows], stats=stats)
+                                          y_stride=y_stride, out=tile[:my_rows], stats=stats)
             if trace_end is not None:
                 trace_end[0].record(streams[slot])
-            if rgba8:
-                rens[slot].quantize(ft[:my_rows], out=tile[:my_rows])
             if gatherer:
                 gatherer.put(1)
         last[0] = slot
@@ -501,30 +497,21 @@ def main():
     def step_batch(k, frame, n, slot=0, stats=False):
         """n frames (frame, frame+1, ...) in one launch of context `slot`; each frame's tile then
         goes to the gatherer (converted / copied into its rotating tile) or stays in the batch buffer."""
-        batch_buf, batch_buf8 = batch_bufs[slot], batch_bufs8[slot]
+        # the launch's frames (RGBA8: written by the library in the texture-write conversion, MM_EXT_RGBA8)
+        buf = batch_bufs8[slot] if rgba8 else batch_bufs[slot]
         with torch.cuda.stream(streams[slot]):
+            tl = bgather.tiles(n) if bgather else None
+            # straight into the gatherer's tile when the rank's rows fill it, else into the batch buffer
+            direct = tl is not None and my_rows == tl.shape[1]
             _, st = rens[slot].trace_tile_frames(u, make_ext(spp, bl, ml, frame=frame), n, 0, y0, W, my_rows,
-                                                 y_stride=y_stride, out=batch_buf[:n], stats=stats)
+                                                 y_stride=y_stride, out=tl if direct else buf[:n], stats=stats)
             if trace_end is not None:  # the launch's end on its stream (exposed-gather clock, N > 1)
                 trace_end[0].record(streams[slot])
-            # the launch's frames are contiguous: one conversion / copy for all of them when the rank's rows fill its
-            # tile (each small per-frame kernel costs a launch gap: ~1 % of a rank's 20-frame launch at N = 8)
             if bgather:
-                tl = bgather.tiles(n)
-                if my_rows == tl.shape[1]:
-                    if rgba8:
-                        rens[slot].quantize(batch_buf[:n], out=tl)
-                    else:
-                        tl.copy_(batch_buf[:n])
-                else:
+                if not direct:
                     for f in range(n):
-                        if rgba8:
-                            rens[slot].quantize(batch_buf[f], out=tl[f][:my_rows])
-                        else:
-                            tl[f][:my_rows].copy_(batch_buf[f])
+                        tl[f][:my_rows].copy_(buf[f])
                 bgather.put(n)
-            elif rgba8:  # every frame delivered in RGBA8
-                rens[slot].quantize(batch_buf[:n], out=batch_buf8[:n])
         last[0] = slot
         return st
 

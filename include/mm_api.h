@@ -110,6 +110,11 @@ int  mm_quantize_rgba8(mm_ctx* ctx, const float* rgba_dev, uint8_t* rgba8_dev, u
  * over any number of GPUs reproduces the 1-GPU image bit for bit.
  * out_dev: caller DEVICE pointer to w*h float4 (row-major over (j,i));
  * alpha = 1 (or, with MM_EXT_ACCUMULATE, += the frame value, alpha += 1).
+ * With MM_EXT_RGBA8 out_dev holds w*h 4-byte RGBA8 pixels instead: the
+ * texture-write conversion of that float4 (mm_quantize_rgba8's, alpha 255),
+ * written by the trace's own resolve (the reference's output texture format,
+ * src/main.rs:702-709, without a float frame in between); not with
+ * MM_EXT_ACCUMULATE.
  * stats: optional host pointer; filled after an implicit sync when
  * MM_EXT_COUNT_STATS is set.  rays and paths are exact; node_visits and
  * rect_tests count the work of the query method that ran (BVH: interior
@@ -121,7 +126,8 @@ int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
 
 /* Several consecutive frames of the same tile in ONE launch: frame f (0 <=
  * f < n_frames) is traced with RNG frame ext->frame + f into out_dev + f*w*h*4
- * (out_dev: n_frames*w*h float4, frame-major); each frame is bit-identical to
+ * (out_dev: n_frames*w*h float4, frame-major; 4-byte pixels with
+ * MM_EXT_RGBA8); each frame is bit-identical to
  * mm_trace_tile(..., frame = ext->frame + f).  The frames share the launch's
  * work queue, so the ~0.4 ms tail in which the last waves finish their last
  * chunks is paid once per launch instead of once per frame (throughput mode

@@ -69,6 +69,9 @@ typedef struct mm_ext {
 /* mm_ext.flags */
 #define MM_EXT_COUNT_STATS   0x1u  /* fill mm_stats (costs a few %)            */
 #define MM_EXT_ACCUMULATE    0x2u  /* out += frame value instead of out = ...  */
+#define MM_EXT_RGBA8         0x4u  /* out holds RGBA8 (4 B per pixel: the texture-write
+                                      conversion of mm_quantize_rgba8, alpha 255)
+                                      instead of float4; not with ACCUMULATE    */
 
 /* Work counters.  A "ray" is one closest-hit BVH query, i.e. one execution
  * of src/shaders.metal:307.                                  */

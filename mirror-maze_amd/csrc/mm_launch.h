@@ -38,7 +38,7 @@ struct TileJob {
     // Fused resolve (wave-persistent kernel, 64 % spp == 0): each wave reduces
     // its chunk's whole pixels in registers and writes out[pixel] itself, in
     // k_resolve's order; no per-sample staging buffer, no resolve launch.
-    float4* out = nullptr;
+    void* out = nullptr;  // float4 per pixel, or RGBA8 (4 B) with MM_EXT_RGBA8 (mm_wave_util.h store_pixel)
     uint32_t fuse = 0;
     // Diagnostics (mm_set_wave_timeline): per wave of the wave-persistent
     // kernel, 4 x u64 = (entry, LDS staged, exit, chunks) in wall_clock64()
@@ -131,6 +131,6 @@ hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32
 hipError_t launch_quantize(const float4* in, uint32_t* out, size_t n, hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
-hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s);
+hipError_t launch_resolve(const TileJob& job, const float4* samples, void* out, hipStream_t s);
 
 }  // namespace mm

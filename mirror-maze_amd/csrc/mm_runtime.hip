@@ -854,6 +854,12 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     if ((uint64_t)x0 + w > W || (uint64_t)y0 + (uint64_t)(h - 1) * y_stride >= H)
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: tile outside the frame");
     if (n_frames == 0) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: no frames");
+    // MM_EXT_RGBA8: 4-byte RGBA8 pixels (the fused texture-write conversion) instead of float4
+    const bool rgba8 = (e->flags & MM_EXT_RGBA8) != 0;
+    if (rgba8 && (e->flags & MM_EXT_ACCUMULATE))
+        return fail(c, MM_ERR_INVALID, "mm_trace_tile: MM_EXT_RGBA8 frames cannot accumulate");
+    const size_t out_bpp = rgba8 ? 4 : 16;
+    if (reinterpret_cast<uintptr_t>(out_dev) % 4) return fail(c, MM_ERR_INVALID, "mm_trace_tile: misaligned output");
     HIPC(c, hipSetDevice(c->device));
     const bool want_stats = (e->flags & MM_EXT_COUNT_STATS) != 0;
     const uint64_t row_paths = (uint64_t)w * e->spp;
@@ -962,7 +968,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         job.fuse = fuse ? 1u : 0u;
         job.wave_ts = c->d_wave_ts;
         job.wave_ts_cap = c->wave_ts_cap;
-        job.out = reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w;
+        job.out = reinterpret_cast<char*>(out_dev) + (size_t)j0 * w * out_bpp;
         job.n_frames = n_frames;
         job.reserve_cus = c->opt_reserve_cus;
         job.fault = (c->opt_fault == 1 || c->opt_fault == 4) ? (uint32_t)c->opt_fault : 0u;
@@ -1029,8 +1035,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         // row batch), so one resolve over h x n_frames rows covers them all
         TileJob rj = job;
         if (defer) rj.h = job.h * n_frames;
-        const hipError_t re =
-            launch_resolve(rj, c->d_samples, reinterpret_cast<float4*>(out_dev) + (size_t)j0 * w, c->stream);
+        const hipError_t re = launch_resolve(rj, c->d_samples, job.out, c->stream);
         if (re != hipSuccess) {
             rc = fail(c, MM_ERR_HIP, std::string("launch_resolve: ") + hipGetErrorString(re));
             break;

@@ -33,8 +33,26 @@ __device__ __forceinline__ void flush_stats(unsigned long long* stats, const Cou
 // operations in the same order as k_resolve, so the pixel is bit-identical.
 // Called by all 64 lanes (uniform control flow); `valid` lanes' pixels written
 // to out (the job's output, or its frame's slice of it in a multi-frame launch).
+// Pixel pix of a launch's output: float4 (alpha 1, or += the frame value with
+// MM_EXT_ACCUMULATE), or with MM_EXT_RGBA8 its texture-write conversion in 4
+// bytes -- mm_quantize_rgba8's (k_quantize) on that float4, fused into the
+// store so the float frame never goes to HBM.
+__device__ __forceinline__ void store_pixel(const TileJob& job, void* __restrict__ out, size_t pix, F3 v) {
+    if (job.e.flags & MM_EXT_RGBA8) {
+        reinterpret_cast<uint32_t*>(out)[pix] =
+            unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | (unorm8(1.0f) << 24);
+    } else if (job.e.flags & MM_EXT_ACCUMULATE) {
+        float4* o = reinterpret_cast<float4*>(out) + pix;
+        const float4 p = *o;
+        *o = make_float4(p.x + v.x, p.y + v.y, p.z + v.z, p.w + 1.0f);
+    } else {
+        reinterpret_cast<float4*>(out)[pix] = make_float4(v.x, v.y, v.z, 1.0f);
+    }
+}
+
+// (out: the launch's output base; pixel path / spp + pix0 of it)
 __device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32_t path, bool valid,
-                                                float4* __restrict__ out) {
+                                                void* __restrict__ out, size_t pix0) {
     const uint32_t spp = job.e.spp, lane = threadIdx.x & 63u;
     F3 acc;
     if (spp % 8 == 0) {
@@ -50,15 +68,8 @@ __device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32
             acc = acc + F3{__shfl(s.x, (int)(lane + k)), __shfl(s.y, (int)(lane + k)), __shfl(s.z, (int)(lane + k))};
     }
     if (valid && (lane & (spp - 1)) == 0) {
-        const uint32_t pix = path / spp;
         const float m = (float)spp;
-        const F3 v = F3{acc.x / m, acc.y / m, acc.z / m};
-        if (job.e.flags & MM_EXT_ACCUMULATE) {
-            const float4 o = out[pix];
-            out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
-        } else {
-            out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
-        }
+        store_pixel(job, out, pix0 + path / spp, F3{acc.x / m, acc.y / m, acc.z / m});
     }
 }
 

@@ -506,7 +506,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             if (!job.fuse) samples[fr * n_paths + path] = make_float4(s.x, s.y, s.z, 0.0f);
             paths++;
         }
-        if (job.fuse) resolve_in_wave(job, s, path, valid, job.out + (size_t)fr * job.w * job.h);
+        if (job.fuse) resolve_in_wave(job, s, path, valid, job.out, (size_t)fr * job.w * job.h);
     }
 #ifdef MM_PHASE_CLOCKS
     {  // the wave's time in queries / shading: the max over its lanes (some lane runs every iteration)
@@ -1106,7 +1106,7 @@ bool ab_variants_built() {
 // ---------------------------------------------------------------------------
 // Sample reduction: spp % 8 == 0 -> pairwise tree in blocks of 8, blocks added
 // left to right (the reference order for 64 spp); otherwise left to right.
-__global__ void k_resolve(TileJob job, const float4* __restrict__ samples, float4* __restrict__ out) {
+__global__ void k_resolve(TileJob job, const float4* __restrict__ samples, void* __restrict__ out) {
     const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= job.w * job.h) return;
     const uint32_t spp = job.e.spp;
@@ -1124,28 +1124,22 @@ __global__ void k_resolve(TileJob job, const float4* __restrict__ samples, float
         for (uint32_t k = 1; k < spp; ++k) acc = acc + xyz(s[k]);
     }
     const float m = (float)spp;
-    const F3 v = F3{acc.x / m, acc.y / m, acc.z / m};
-    if (job.e.flags & MM_EXT_ACCUMULATE) {
-        float4 o = out[pix];
-        out[pix] = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + 1.0f);
-    } else {
-        out[pix] = make_float4(v.x, v.y, v.z, 1.0f);
-    }
+    store_pixel(job, out, pix, F3{acc.x / m, acc.y / m, acc.z / m});
 }
 
 // The same reduction when 64 % spp == 0, a wave per 64 consecutive samples
 // (64/spp whole pixels): every load is one coalesced 1-KB wave access, and
 // resolve_in_wave adds in k_resolve's order (bit-identical).
 __global__ __launch_bounds__(256) void k_resolve_wave(TileJob job, const float4* __restrict__ samples,
-                                                      float4* __restrict__ out) {
+                                                      void* __restrict__ out) {
     const uint32_t n = job.w * job.h * job.e.spp;
     const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;  // waves never straddle the end: n % 64 == 0
     const bool valid = path < n;                                   // unless the tile is ragged
     const float4 v = valid ? samples[path] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    resolve_in_wave(job, F3{v.x, v.y, v.z}, path, valid, out);
+    resolve_in_wave(job, F3{v.x, v.y, v.z}, path, valid, out, 0);
 }
 
-hipError_t launch_resolve(const TileJob& job, const float4* samples, float4* out, hipStream_t s) {
+hipError_t launch_resolve(const TileJob& job, const float4* samples, void* out, hipStream_t s) {
     const uint32_t n = job.w * job.h;
     if (64 % job.e.spp == 0) {
         const uint32_t paths = n * job.e.spp;

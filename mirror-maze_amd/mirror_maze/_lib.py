@@ -31,7 +31,7 @@ class MMError(RuntimeError):
 
 MM_OK, MM_ERR_INVALID, MM_ERR_HIP, MM_ERR_NOMEM = 0, -1, -2, -3
 MM_ERR_NO_SCENE, MM_ERR_STACK, MM_ERR_UNSUPPORTED = -4, -5, -6
-MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE = 0x1, 0x2
+MM_EXT_COUNT_STATS, MM_EXT_ACCUMULATE, MM_EXT_RGBA8 = 0x1, 0x2, 0x4
 MM_PIPE_AUTO, MM_PIPE_MEGAKERNEL, MM_PIPE_WAVEFRONT, MM_PIPE_REFERENCE = 0, 1, 2, 3
 MM_OPT_LDS_NODES, MM_OPT_BLOCK, MM_OPT_PERSIST, MM_OPT_TRAVERSAL, MM_OPT_LDS_RECTS = 1, 2, 3, 7, 8
 MM_OPT_LDS_SPLIT, MM_OPT_FUSE_RESOLVE, MM_OPT_RESERVE_CUS, MM_OPT_DICT_NODES, MM_OPT_DEFER = 9, 12, 19, 20, 21

@@ -149,42 +149,54 @@ class Renderer:
         return out
 
     # -- throughput mode ------------------------------------------------------
-    def trace_tile(self, uniform: _lib.mm_uniform, ext: _lib.mm_ext, x0: int, y0: int, w: int, h: int,
-                   y_stride: int = 1, out=None, stats: bool = False):
-        """Render a tile into a (h, w, 4) float32 CUDA tensor (allocated if None).
-        Returns (out, mm_stats or None)."""
+    @staticmethod
+    def _out(out, shape, rgba8, device):
+        """The output tensor: float32 (..., 4), or uint8 (..., 4) for RGBA8
+        frames (MM_EXT_RGBA8, set when `out` is uint8 or rgba8=True)."""
         import torch
 
         if out is None:
-            out = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{self.device}")
-        if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous() and out.numel() == h * w * 4):
-            raise ValueError("out must be a contiguous float32 CUDA tensor of h*w*4 elements")
+            out = torch.zeros(shape, dtype=torch.uint8 if rgba8 else torch.float32, device=device)
+        n = 1
+        for d in shape:
+            n *= d
+        if not (out.is_cuda and out.dtype in (torch.float32, torch.uint8) and out.is_contiguous()
+                and out.numel() == n):
+            raise ValueError(f"out must be a contiguous float32 or uint8 CUDA tensor of {n} elements")
+        return out, out.dtype == torch.uint8
+
+    def trace_tile(self, uniform: _lib.mm_uniform, ext: _lib.mm_ext, x0: int, y0: int, w: int, h: int,
+                   y_stride: int = 1, out=None, stats: bool = False, rgba8: bool = False):
+        """Render a tile into a (h, w, 4) float32 CUDA tensor (allocated if None),
+        or with rgba8 / a uint8 `out` its RGBA8 texture-write conversion
+        (MM_EXT_RGBA8: equal to quantize() of the float tile).  Returns (out,
+        mm_stats or None)."""
+        import torch
+
+        out, r8 = self._out(out, (h, w, 4), rgba8, f"cuda:{self.device}")
         if not self._pinned_stream:  # order with the torch ops that made / read `out`
             self._check(lib().mm_set_stream(self._ctx, torch.cuda.current_stream(out.device).cuda_stream))
         e = _lib.mm_ext(ext.spp, ext.bounce_limit, ext.mirror_limit, ext.frame,
-                        ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0), 0)
+                        ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0) | (_lib.MM_EXT_RGBA8 if r8 else 0), 0)
         st = _lib.mm_stats()
         self._check(lib().mm_trace_tile(self._ctx, C.byref(uniform), C.byref(e), x0, y0, w, h, y_stride,
                                         out.data_ptr(), C.byref(st)))
         return out, (st if stats else None)
 
     def trace_tile_frames(self, uniform: _lib.mm_uniform, ext: _lib.mm_ext, n_frames: int, x0: int, y0: int,
-                          w: int, h: int, y_stride: int = 1, out=None, stats: bool = False):
+                          w: int, h: int, y_stride: int = 1, out=None, stats: bool = False, rgba8: bool = False):
         """Render frames ext.frame .. ext.frame + n_frames - 1 of a tile in ONE
         launch (mm_trace_tile_frames) into a (n_frames, h, w, 4) float32 CUDA
-        tensor (allocated if None); frame f equals trace_tile with frame
-        ext.frame + f.  Returns (out, mm_stats summed over the frames or None)."""
+        tensor (allocated if None; uint8 RGBA8 with rgba8 / a uint8 `out`, as
+        trace_tile); frame f equals trace_tile with frame ext.frame + f.
+        Returns (out, mm_stats summed over the frames or None)."""
         import torch
 
-        if out is None:
-            out = torch.zeros((n_frames, h, w, 4), dtype=torch.float32, device=f"cuda:{self.device}")
-        if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()
-                and out.numel() == n_frames * h * w * 4):
-            raise ValueError("out must be a contiguous float32 CUDA tensor of n_frames*h*w*4 elements")
+        out, r8 = self._out(out, (n_frames, h, w, 4), rgba8, f"cuda:{self.device}")
         if not self._pinned_stream:
             self._check(lib().mm_set_stream(self._ctx, torch.cuda.current_stream(out.device).cuda_stream))
         e = _lib.mm_ext(ext.spp, ext.bounce_limit, ext.mirror_limit, ext.frame,
-                        ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0), 0)
+                        ext.flags | (_lib.MM_EXT_COUNT_STATS if stats else 0) | (_lib.MM_EXT_RGBA8 if r8 else 0), 0)
         st = _lib.mm_stats()
         self._check(lib().mm_trace_tile_frames(self._ctx, C.byref(uniform), C.byref(e), n_frames, x0, y0, w, h,
                                                y_stride, out.data_ptr(), C.byref(st)))

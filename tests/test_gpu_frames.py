@@ -259,3 +259,44 @@ def test_camera_sweep(gpu, maze_n, bl, ml):
         assert _diff(got.cpu().numpy(), ref) == 0, (cx, cz, d)
         assert st.rays == n
     r.close()
+
+
+@pytest.mark.parametrize("case", ["c3-two-frames-rings", "c3-two-frames-fused", "c2-frame", "spp3-strided"])
+def test_rgba8_frames_equal_the_quantized_float_frames(gpu, case):
+    """MM_EXT_RGBA8: the trace writes each pixel's texture-write conversion
+    itself (the fused resolve in the wave, the staged resolve after the tail
+    rings, and the per-pixel resolve for spp that does not divide 64); every
+    byte equals mm_quantize_rgba8 of the float frame the same call writes
+    without the flag (whose floats the other tests hold to the oracle)."""
+    import torch
+
+    from mirror_maze import MM_EXT_ACCUMULATE, MMError, Renderer, default_uniform, make_ext
+
+    r = Renderer(0)
+    n_maze, W, H, spp, bl, ml = {"c3-two-frames-rings": (32, 1920, 1080, 8, 8, 8),
+                                 "c3-two-frames-fused": (32, 1920, 1080, 8, 8, 8),
+                                 "c2-frame": (16, 1920, 1080, 1, 4, 15),
+                                 "spp3-strided": (16, 640, 480, 3, 4, 15)}[case]
+    r.upload_scene(_scene(n_maze))
+    if case == "c3-two-frames-rings":
+        r.set_option(21, 32)
+        r.set_option(22, 1 << 24)
+    elif case == "c3-two-frames-fused":
+        r.set_option(21, 0)
+    u, e = default_uniform(W, H, 0), make_ext(spp, bl, ml, frame=7)
+    if case.startswith("c3"):
+        f32, _ = r.trace_tile_frames(u, e, 2, 0, 0, W, H)
+        u8, _ = r.trace_tile_frames(u, e, 2, 0, 0, W, H, rgba8=True)
+    elif case == "c2-frame":
+        f32, _ = r.trace_tile(u, e, 0, 0, W, H)
+        u8, _ = r.trace_tile(u, e, 0, 0, W, H, rgba8=True)
+    else:  # every 7th row from row 3, a ragged 61-row tile
+        f32, _ = r.trace_tile(u, e, 5, 3, 600, 61, y_stride=7)
+        u8 = torch.zeros((61, 600, 4), dtype=torch.uint8, device="cuda")
+        r.trace_tile(u, e, 5, 3, 600, 61, y_stride=7, out=u8)
+    want = r.quantize(f32)
+    torch.cuda.synchronize()
+    assert u8.dtype == torch.uint8 and torch.equal(u8, want), case
+    with pytest.raises(MMError):
+        r.trace_tile(u, make_ext(spp, bl, ml, flags=MM_EXT_ACCUMULATE), 0, 0, 64, 8, rgba8=True)
+    r.close()
