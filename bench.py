@@ -114,6 +114,11 @@ def parse():
     p.add_argument("--accumulate", action="store_true",
                    help="temporal accumulation (C5): every frame adds into one running sum per rank "
                         "(MM_EXT_ACCUMULATE) and the frame is gathered once, after the last step")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="diagnostics: the N ranks all use GPU 0 and their tiles reach rank 0 as host copies over "
+                        "torch.distributed (gloo) into mm_assemble_rows (mirror_maze.comm.HostComm; RCCL allows "
+                        "one rank per GPU) -- the rest of the N-GPU path runs unchanged; its timing is not a "
+                        "measurement (VERDICT r05 item 2)")
     p.add_argument("--emulate-ranks", type=int, default=0,
                    help="diagnostics on one GPU: trace only rank 0's row set of an N-rank split")
     p.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
@@ -268,23 +273,33 @@ def cpu_baseline(scene, u, ext, W, H, budget_s):
             "host_cpus": os.cpu_count()}
 
 
-def pmc_profile(args, frames_per_launch, k_avg_s, world):
-    """Measured counters of the dominant kernel from profiles/pmc_<config>.json
-    (pmc_<config>_r<N>.json for --emulate-ranks N; scripts/pmc_record.py over
-    rocprofv3 --pmc passes of bench.py's own launch), used only when its source
-    hash is this tree's.  Returns
-    (measured dict, HBM bytes per launch or None)."""
-    # rank 0's share of an N-way split (--emulate-ranks N) has its own launch shape: pmc_<config>_r<N>.json
-    name = args.config + (f"_r{args.emulate_ranks}" if args.emulate_ranks and args.emulate_ranks > 1 else "")
-    f = REPO / "profiles" / f"pmc_{name}.json"
-    if not f.exists() or args.pipeline != "auto" or args.opt or world > 1:
-        return {"source": None, "note": "no PMC profile for this configuration"}, None
+def pmc_record_name(config: str, ranks: int) -> str:
+    """profiles/pmc_<name>.json of a launch shape: the configuration's whole
+    frames at N = 1, rank 0's row set of an N-way split otherwise (the shape
+    rank 0 runs at world = N, and --emulate-ranks N on one GPU)."""
+    return config + (f"_r{ranks}" if ranks > 1 else "")
+
+
+def pmc_profile(args, frames_per_launch, k_avg_s, world, shared=False):
+    """Measured counters of the dominant kernel from profiles/pmc_<name>.json
+    (scripts/pmc_record.py over rocprofv3 --pmc passes of bench.py's own
+    launch), used only when its source hash is this tree's.  The record is
+    the launch shape rank 0 runs: pmc_<config>.json at N = 1,
+    pmc_<config>_r<N>.json at world = N > 1 and for --emulate-ranks N, so the
+    N-GPU lines' headline is the same quantity as N = 1's (VERDICT r05 item
+    1).  Returns (measured dict, HBM bytes per launch or None)."""
+    if shared:
+        return {"source": None, "note": "diagnostics (--shared-gpu): N ranks share one GPU, no roofline"}, None
+    ranks = world if world > 1 else (args.emulate_ranks if args.emulate_ranks > 1 else 1)
+    f = REPO / "profiles" / f"pmc_{pmc_record_name(args.config, ranks)}.json"
+    if not f.exists() or args.pipeline != "auto" or args.opt:
+        return {"source": None, "note": f"no PMC record for this launch shape ({f.relative_to(REPO)}, default "
+                                        f"options)"}, None
     rec = json.loads(f.read_text())
     here = src_hash()
     if rec.get("src_hash") != here:
         # other kernel sources: only its executed lane-ops per frame, scaled to this run's frames per launch, is
-        # offered (labelled) as the headline's basis -- closer to what the kernel executes than the
-        # reference-walk model; its HBM bytes are not used
+        # offered (labelled) beside a null headline; its HBM bytes are not used
         stale = {"source": str(f.relative_to(REPO)), "stale": True, "profile_src_hash": rec.get("src_hash"),
                  "src_hash": here, "note": "profile of other kernel sources: HBM bytes not used"}
         if rec.get("valu_lane_ops_per_launch") and rec.get("frames_per_launch"):
@@ -312,34 +327,34 @@ def pmc_profile(args, frames_per_launch, k_avg_s, world):
 
 def roofline(ops, alg_bytes, k_avg_s, k_launches, frames_per_launch, measured, traffic, contexts, kern_res):
     """The dominant kernel's roofline object.  Headline (achieved / frac): the
-    hardware's executed fp32 VALU lane-ops per launch from the same-source PMC
-    record (SQ_INSTS_VALU x 64 x lane utilisation) / this run's mean launch
-    time, against 78.6 T lane-ops/s.  Without a PMC
-    record of these sources the headline falls back to a record of other
-    sources (its lane-ops per frame, labelled STALE in "basis"), else to the
-    reference-walk model, and says so in "basis".  The reference-walk VALU model and the
-    136 B/ray HBM model are kept as labelled sub-objects."""
+    hardware's executed VALU lane-ops per launch (fp32, integer, compare and
+    select alike) from the same-source PMC record of this launch shape
+    (SQ_INSTS_VALU x 64 x lane utilisation) / this run's mean launch time,
+    against 78.6 T lane-ops/s.  Without such a record
+    achieved / frac are null and "basis" says why -- never a model (VERDICT
+    r05 item 1).  The reference-walk VALU model and the 136 B/ray HBM model
+    are labelled sub-objects with a "model_ratio" (a model's count over the
+    peak, which can pass 1 -- not a measured fraction)."""
     ref_tops = ops / k_avg_s / 1e12
     lane_tops = measured.get("valu_lane_ops_tops") if isinstance(measured, dict) else None
     stale_tops = measured.get("stale_valu_lane_ops_tops") if isinstance(measured, dict) else None
     hw = lane_tops is not None
-    # without a PMC record of THESE sources the headline is the reference-walk model, never another build's
-    # counters (ADVICE r04); a stale record's lane-ops rate is kept only in its own labelled sub-object
-    achieved = lane_tops if hw else ref_tops
     return {
-        "bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": traffic,
+        "bound": "valu", "achieved": round(lane_tops, 3) if hw else None, "peak": VALU_PEAK_TOPS,
+        "unit": "T lane-ops/s",
+        "frac": round(lane_tops / VALU_PEAK_TOPS, 4) if hw else None, "traffic": traffic,
         "stale": (not hw) and stale_tops is not None,
-        "basis": ("executed fp32 VALU lane-ops (PMC: SQ_INSTS_VALU x 64 x SQ_THREAD_CYCLES_VALU / "
-                  "(64 SQ_ACTIVE_INST_VALU), profiles/pmc_<config>.json of these sources) per launch / mean "
-                  "launch time" if hw else
-                  "reference_equivalent: no PMC record of these sources (see reference_equivalent)"),
-        "stale_profile": ({"valu_lane_ops_tops": stale_tops, "frac": round(stale_tops / VALU_PEAK_TOPS, 4),
+        "basis": ("executed VALU lane-ops (PMC: SQ_INSTS_VALU x 64 x SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU), "
+                  f"{measured.get('source')} of these sources, this launch shape) per launch / mean launch time"
+                  if hw else
+                  "none: " + (measured.get("note") or "no PMC record of these sources") +
+                  " -- achieved / frac null (the models below are not measurements)"),
+        "stale_profile": ({"valu_lane_ops_tops": stale_tops, "model_ratio": round(stale_tops / VALU_PEAK_TOPS, 4),
                            "note": "executed lane-ops per frame of the PMC record of OTHER kernel sources "
                                    "(measured.profile_src_hash) x this run's frames per launch / mean launch "
                                    "time -- not measured on these sources"}
                           if (not hw) and stale_tops is not None else None),
-        "peak_basis": "256 CU x 4 SIMD x 32 fp32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md)",
+        "peak_basis": "256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md)",
         "kernel": "k_trace_wavepersist", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
         "launches": k_launches, "frames_per_launch": round(frames_per_launch, 3),
         "timing": ("HIP events around each launch on its stream" +
@@ -347,15 +362,17 @@ def roofline(ops, alg_bytes, k_avg_s, k_launches, frames_per_launch, measured, t
                     "span includes time shared with its neighbours" if contexts > 1 else "")),
         "kernel_resources": kern_res,
         "reference_equivalent": {
-            "achieved": round(ref_tops, 3), "frac": round(ref_tops / VALU_PEAK_TOPS, 4),
-            "ops": ("fp32 VALU lane-ops the reference BVH walk would execute on the timed frames (SURVEY 8d "
+            "lane_ops_tops": round(ref_tops, 3), "model_ratio": round(ref_tops / VALU_PEAK_TOPS, 4),
+            "ops": ("VALU lane-ops the reference BVH walk would execute on the timed frames (SURVEY 8d "
                     "model: 25 per AABB test + 71 per rect test, counted by the BVH loop form) per launch / "
-                    "mean launch time: useful work per second, not what this kernel executes")},
+                    "mean launch time: useful work per second, not what this kernel executes (it passes 1 "
+                    "where the grid search does far less work than the walk)")},
         "model_hbm": {"bytes_per_ray": BYTES_PER_RAY, "bytes_per_launch": round(alg_bytes),
-                      "achieved_gbs": round(alg_bytes / k_avg_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
-                      "frac": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                      "gbs": round(alg_bytes / k_avg_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+                      "model_ratio": round(alg_bytes / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                       "note": ("SURVEY 8(d) accounting model of a SoA wavefront (136 B/ray + 16 "
-                               "B/px), not traffic: the megakernel keeps path state in registers")},
+                               "B/px), not traffic: the megakernel keeps path state in registers and never "
+                               "moves these bytes (measured traffic: roofline.traffic / measured)")},
         "measured": measured,
     }
 
@@ -384,7 +401,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     # under torchrun (even with one rank) the frame goes through the RCCL gather path; torch.distributed (gloo,
     # CPU) is only the rendezvous, the barriers and the timing reductions -- the frames move through the
     # library's own RCCL communicator (include/mm_comm.h)
@@ -420,7 +437,11 @@ def main():
     streams = [r.own_stream() for r in rens]
     u = default_uniform(W, H, 0)
     comm = None
-    if distributed:  # the library's RCCL communicator: rank 0's unique id over the gloo rendezvous
+    if distributed and args.shared_gpu:  # diagnostics: every rank on GPU 0, tiles over gloo (HostComm)
+        from mirror_maze.comm import HostComm
+
+        comm = HostComm(rens[0], world, rank)
+    elif distributed:  # the library's RCCL communicator: rank 0's unique id over the gloo rendezvous
         from mirror_maze.comm import Comm
 
         uid = [Comm.unique_id(rens[0]) if rank == 0 else None]
@@ -680,11 +701,20 @@ def main():
         dist.all_reduce(k_lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(k_hi, op=dist.ReduceOp.MAX)
         n_gathers = gatherer.launch
+        from mirror_maze.comm import Comm
+
         dist_info = {
-            "rccl_world": comm.n_ranks, "rccl_version": Comm.rccl_version(),
-            "backend": ("RCCL through libmirror_maze.so (mm_comm_init_rank + mm_gather_rows: ncclSend/ncclRecv "
-                        "to rank 0, de-interleave kernel); torch.distributed " + str(dist.get_backend()) +
-                        " for the rendezvous, barriers and timing reductions"),
+            "rccl_world": None if args.shared_gpu else comm.n_ranks,
+            "rccl_version": None if args.shared_gpu else Comm.rccl_version(),
+            "rccl_header_version": Comm.rccl_header_version(),
+            "shared_gpu": bool(args.shared_gpu),
+            "backend": (("DIAGNOSTICS (--shared-gpu): every rank on GPU 0; tiles to rank 0 as host copies over "
+                         "torch.distributed gloo send/recv, de-interleaved by mm_assemble_rows (mirror_maze.comm."
+                         "HostComm) -- the rest of the N-GPU path unchanged; timings not a measurement")
+                        if args.shared_gpu else
+                        ("RCCL through libmirror_maze.so (mm_comm_init_rank + mm_gather_rows: ncclSend/ncclRecv "
+                         "to rank 0, de-interleave kernel); torch.distributed " + str(dist.get_backend()) +
+                         " for the rendezvous, barriers and timing reductions")),
             "torch_distributed_world": dist.get_world_size(),
             "kernel_ms_per_rank": {"rank0": round(k_ms, 3), "min": round(float(k_lo[0]), 3),
                                    "max": round(float(k_hi[0]), 3)},
@@ -711,7 +741,7 @@ def main():
         ops = (OPS_PER_AABB * 2 * visits + OPS_PER_RECT * rtests) * per_launch   # reference-walk VALU model
         alg_bytes = (BYTES_PER_RAY * rays + BYTES_PER_PIXEL * my_rows * W * args.steps) * per_launch
         frames_per_launch = args.steps * per_launch
-        measured, traffic = pmc_profile(args, frames_per_launch, k_avg_s, world)
+        measured, traffic = pmc_profile(args, frames_per_launch, k_avg_s, world, shared=args.shared_gpu)
         line = {
             "metric": "Mrays/sec + ms/frame at 1920x1080, 8 spp, 8 bounces; 1/2/4/8-GPU scaling",
             "value": round(value, 2),
@@ -728,7 +758,9 @@ def main():
             "data": "synthetic: Kruskal maze seed 0 (host C++ restatement), default camera, RNG keyed (pixel,sample,frame)",
             "config": {"workload": desc, "maze_n": maze_n, "width": W, "height": H, "spp": spp,
                        "bounce_limit": bl, "mirror_limit": ml, "pipeline": args.pipeline,
-                       "parallelism": (f"rows interleaved x{world} + RCCL gather" if distributed else "1 GPU") +
+                       "parallelism": ((f"rows interleaved x{world} ranks on ONE GPU + host gather (diagnostics)"
+                                        if args.shared_gpu else f"rows interleaved x{world} + RCCL gather")
+                                       if distributed else "1 GPU") +
                                       (f" (emulating rank 0 of {args.emulate_ranks})" if args.emulate_ranks > 1 else ""),
                        "frame_contexts": active[0],
                        "frame_format": "rgba8" if rgba8 else "f32",
@@ -738,6 +770,7 @@ def main():
                        "frame_contexts_calibration_ms": ({str(k): round(v, 3) for k, v in calib.items()}
                                                          if calib else None),
                        "rays_per_frame": int(rays_all / args.steps), "paths_per_frame": int(paths_all / args.steps),
+                       "rays_total": int(rays_all),
                        "node_visits_per_ray": round(visits_all / max(rays_all, 1), 2),
                        "rect_tests_per_ray": round(rtests_all / max(rays_all, 1), 2)},
             "roofline": roofline(ops, alg_bytes, k_avg_s, k_launches, frames_per_launch, measured, traffic,

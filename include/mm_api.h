@@ -151,7 +151,7 @@ int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
                                   (SoA state in HBM, one extend/shade launch pair per bounce) measured
                                   ~45 ms vs 5.7 ms per C3 frame and was retired (DESIGN.md §4,
                                   profiles/r02/wavefront_pmc.txt) */
-#define MM_PIPE_REFERENCE  3   /* straight statement of the reference kernel
+#define MM_PIPE_REFERENCE  3   /* straight statement of the reference kernel, one thread per path
                                   (IEEE division everywhere); A/B baseline  */
 int  mm_set_pipeline(mm_ctx* ctx, int pipe);
 
@@ -161,32 +161,30 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
  * neutral: 4, 5, 6, 10, 11, 13-17) return MM_ERR_INVALID. */
 #define MM_OPT_LDS_NODES   1   /* 1: stage scene data (BVH or grid) in LDS where it fits (default), 0: read
                                   everything through L1/L2 */
-#define MM_OPT_BLOCK       2   /* threads per workgroup of the one-thread-per-path kernel (64..1024, x64) */
+#define MM_OPT_BLOCK       2   /* threads per workgroup of MM_PIPE_REFERENCE's one-thread-per-path kernel
+                                  (64..1024, x64) */
 #define MM_OPT_PERSIST     3   /* 2: wave-persistent kernel, 64-path chunks, pixels resolved in the wave
-                                  (default), 0: one thread per path (k_trace_mega) */
+                                  (default, the only one); 0 (one thread per path) was removed in round 6:
+                                  MM_ERR_UNSUPPORTED */
 #define MM_OPT_TRAVERSAL   7   /* closest-hit query of the wave-persistent kernel:
                                   -1 auto (default): 11 when the scene allows it, else 7 when every rect has a
                                      compact record, else 5;
                                   11 certified grid search (mm_grid.h): same answer as the reference's BVH walk,
                                      which runs instead on ties / failed certificates / rays outside the grid;
-                                  0 the reference's BVH loop, one step per iteration (nodes in LDS only);
+                                  0 (the reference's BVH loop form) was removed in round 6: MM_ERR_UNSUPPORTED
+                                    (the parity-mode kernel, mm_trace_chunks, still walks it);
                                   5 BVH, leaf tests and the next interior step in one iteration;
                                   7 form 5 with branch-free compact leaf tests (scenes without SLOW records) */
 #define MM_OPT_LDS_RECTS   8   /* BVH forms: 1 compact rect records in LDS beside the nodes when both fit (default) */
-#define MM_OPT_LDS_SPLIT   9   /* BVH forms, nodes larger than the LDS budget: cache the top of the
-                                  (breadth-first) node array in LDS, rest via L1/L2.  0 off, 1 auto size where
-                                  dictionary nodes do not fit (default), >1: always a cache of this many KB
-                                  (wins over MM_OPT_DICT_NODES 1) */
+#define MM_OPT_LDS_SPLIT   9   /* removed in round 6 (the top-of-tree node cache measured slower): 0 / 1 are
+                                  accepted and select nothing, > 1 returns MM_ERR_UNSUPPORTED */
 #define MM_OPT_FUSE_RESOLVE 12 /* wave-persistent kernel: 1 reduce each pixel's samples inside the wave
                                   that traced them when 64 % spp == 0 (default), 0 separate k_resolve */
 #define MM_OPT_RESERVE_CUS 19 /* wave-persistent kernel: launch that many CUs' worth of resident blocks
                                   fewer (0..128), so kernels of other streams -- a collective moving the
                                   previous frames -- find free CUs while it runs; 0 default */
-#define MM_OPT_DICT_NODES 20  /* BVH forms 5/7: BVH nodes dictionary-coded (8-bit indices into the scene's
-                                  <= 256 distinct bound values, 12 B per node) so the whole tree sits in LDS:
-                                  1 when the plain nodes do not fit and no explicit split size is set (default),
-                                  2 always when it fits (tests), 0 off.  Read by mm_upload_scene: with 0 there
-                                  the dictionary is not built (MM_INFO_DICT_OK 0) until the next upload */
+#define MM_OPT_DICT_NODES 20  /* removed in round 6 (dictionary-coded BVH nodes measured slower): 0 / 1 are
+                                  accepted and select nothing, 2 returns MM_ERR_UNSUPPORTED */
 #define MM_OPT_DEFER      21  /* wave-persistent kernel: once at most this many lanes of a wave still trace
                                   (past bounce_limit only mirror-hit paths run on), those paths' states go to
                                   their block's tail ring (512 entries) and the block's waves take 64 of them at
@@ -221,11 +219,10 @@ int  mm_set_pipeline(mm_ctx* ctx, int pipe);
                                   4 the launch's first deferred path is lost (its ring entry is reserved,
                                   never written): its reader times out after the normal bound and every
                                   later protocol wait of the launch gives up within 256 polls */
-/* Default builds hold the kernels MM_PIPE_AUTO can select; values that need
- * the A/B-only variants (MM_OPT_PERSIST 0, MM_OPT_TRAVERSAL 0,
+/* The library holds the kernels MM_PIPE_AUTO can select; the values that chose
+ * the variants removed in round 6 (MM_OPT_PERSIST 0, MM_OPT_TRAVERSAL 0,
  * MM_OPT_LDS_SPLIT > 1, MM_OPT_DICT_NODES 2, BVH form 7 without nodes +
- * records in LDS) return MM_ERR_UNSUPPORTED unless the library was built with
- * `make EXTRA=-DMM_AB_VARIANTS` (mm_version() then ends in "+ab"). */
+ * records in LDS) return MM_ERR_UNSUPPORTED. */
 int  mm_set_option(mm_ctx* ctx, int key, int value);
 
 /* Facts about the uploaded scene's search structures (double-valued):
@@ -236,14 +233,16 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
  *   MM_INFO_GRID_INDEX_BYTES its cells + lists part
  *   MM_INFO_LEAN             1 if every rect has a compact record
  *   MM_INFO_DEPTH            BVH depth (max traversal stack entries)
- *   MM_INFO_DICT_OK          1 if the nodes have <= 256 distinct bound values (dictionary nodes possible)
+ *   MM_INFO_DICT_OK          0 (dictionary-coded nodes were removed in round 6; the key is kept)
  *   MM_INFO_LAST_FORM        query method of the last wave-persistent launch (MM_OPT_TRAVERSAL value)
- *   MM_INFO_LAST_LDS_MODE    its LDS mode (trace_kernels.hip: 0, 1, 3, 6, 7, 10 BVH; 11-13 grid)
+ *   MM_INFO_LAST_LDS_MODE    its LDS mode (trace_kernels.hip: 0, 1, 3 BVH; 11-14 grid)
  *   MM_INFO_GRID_FACES       1 if the grid cells carry per-face list ranges (64-bit cell words)
  *   MM_INFO_LAST_DEFER       1 if the last mm_trace_tile* call ran the mirror-tail rings
  *   MM_INFO_LAST_VGPRS       VGPRs per lane of the last wave-persistent kernel (code-object metadata)
  *   MM_INFO_LAST_SCRATCH     its private (scratch) bytes per lane: VGPR spills + traversal stack
- *   MM_INFO_LAST_STATIC_LDS  its static LDS bytes per block (the tail ring's words) */
+ *   MM_INFO_LAST_STATIC_LDS  its static LDS bytes per block (the tail ring's words)
+ *   MM_INFO_GRID_LDS_CAP     bytes the grid placements 11 / 14 stage into (their static LDS array without
+ *                            tail rings; the grid builder's budget: no grid image is built larger) */
 #define MM_INFO_GRID_OK          1
 #define MM_INFO_GRID_CELLS_X     2
 #define MM_INFO_GRID_CELLS_Y     3
@@ -261,6 +260,7 @@ int  mm_set_option(mm_ctx* ctx, int key, int value);
 #define MM_INFO_LAST_VGPRS       15
 #define MM_INFO_LAST_SCRATCH     16
 #define MM_INFO_LAST_STATIC_LDS  17
+#define MM_INFO_GRID_LDS_CAP     18
 int  mm_scene_info(const mm_ctx* ctx, int key, double* value);
 
 /* Diagnostics: record, for every wave of the wave-persistent kernel, four u64

@@ -55,8 +55,15 @@ int mm_comm_init_all(int n, mm_ctx* const* ctxs, mm_comm** out);
 /* rank, n_ranks and HIP device of a communicator (any pointer may be NULL). */
 int mm_comm_info(const mm_comm* comm, int* rank, int* n_ranks, int* device);
 
-/* The RCCL version the library runs against (ncclGetVersion, e.g. 22606). */
+/* The RCCL version the library runs against (ncclGetVersion, e.g. 22606: in a
+ * process that already mapped an RCCL -- torch's -- the loader reuses it by
+ * soname), and the version of the rccl.h it was compiled with (e.g. 22707).
+ * mm_comm_init_rank / mm_comm_init_all refuse (MM_ERR_UNSUPPORTED, both
+ * versions named) a runtime of another major version or older than 2.18: the
+ * calls used here (unique id, init rank / all, send / recv in groups, version
+ * and error strings, destroy) keep their ABI across NCCL 2.18+. */
 int mm_comm_rccl_version(void);
+int mm_comm_rccl_header_version(void);
 
 void mm_comm_destroy(mm_comm* comm);
 

@@ -66,6 +66,22 @@ __global__ __launch_bounds__(256) void k_assemble_rows(const uint8_t* __restrict
 
 bool aligned(const void* p, size_t a) { return reinterpret_cast<uintptr_t>(p) % a == 0; }
 
+// the library is compiled against /opt/rocm's rccl.h but, in a
+// process that mapped another librccl.so first (torch's), runs against that
+// one.  The entry points used here are NCCL 2.x's stable ABI from 2.18 on;
+// another major version, or an older runtime, is refused by name.
+constexpr int kRcclMinVersion = 21800;
+int check_rccl_runtime(mm_ctx* c, const char* who) {
+    int v = 0;
+    if (ncclGetVersion(&v) != ncclSuccess) return ctx_fail(c, MM_ERR_HIP, std::string(who) + ": ncclGetVersion failed");
+    if (v / 10000 != NCCL_VERSION_CODE / 10000 || v < kRcclMinVersion)
+        return ctx_fail(c, MM_ERR_UNSUPPORTED,
+                        std::string(who) + ": RCCL runtime " + std::to_string(v) + " is not ABI-compatible with the "
+                        "rccl.h " + std::to_string(NCCL_VERSION_CODE) + " the library was built with (needs major " +
+                        std::to_string(NCCL_VERSION_CODE / 10000) + ", >= " + std::to_string(kRcclMinVersion) + ")");
+    return MM_OK;
+}
+
 int launch_assemble(mm_ctx* c, const uint8_t* staging, const uint8_t* self, uint8_t* frame, uint32_t n_ranks,
                     uint32_t n_frames, uint32_t rows_max, uint32_t height, size_t row_bytes) {
     const dim3 grid(height, n_frames), block(256);
@@ -97,14 +113,29 @@ int check_shape(mm_ctx* c, const char* who, uint32_t n_ranks, uint32_t n_frames,
     return MM_OK;
 }
 
-// Rank 0's receive staging: n_ranks slabs of one tile set each.
+// Rank 0's receive staging: n_ranks slabs of one tile set each, used by one
+// gather at a time: the stream of this gather waits for the previous gather's
+// assembly (it may have run on another stream), and a regrow frees the old
+// buffer only once that assembly is done.
 int ensure_staging(mm_ctx* c, size_t bytes) {
+    if (!c->gather_done) HIPC(c, hipEventCreateWithFlags(&c->gather_done, hipEventDisableTiming));
+    if (c->gather_pending) HIPC(c, hipStreamWaitEvent(c->stream, c->gather_done, 0));
     if (c->d_gather && c->gather_cap >= bytes) return MM_OK;
+    if (c->gather_pending) HIPC(c, hipEventSynchronize(c->gather_done));
     (void)hipFree(c->d_gather);
     c->d_gather = nullptr;
     c->gather_cap = 0;
     HIPC(c, hipMalloc((void**)&c->d_gather, std::max<size_t>(bytes, 16)));
     c->gather_cap = bytes;
+    return MM_OK;
+}
+
+// After a gather's assembly: mark the staging busy until this point of the
+// gather's stream (only when the gather used it).
+int staging_released(mm_ctx* c, bool used) {
+    if (!used) return MM_OK;
+    HIPC(c, hipEventRecord(c->gather_done, c->stream));
+    c->gather_pending = true;
     return MM_OK;
 }
 
@@ -141,6 +172,7 @@ int mm_comm_init_rank(mm_ctx* c, int n_ranks, int rank, const uint8_t id[MM_COMM
     if (!c || !id || !out) return MM_ERR_INVALID;
     *out = nullptr;
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return ctx_fail(c, MM_ERR_INVALID, "mm_comm_init_rank: bad rank");
+    if (int rc = check_rccl_runtime(c, "mm_comm_init_rank")) return rc;
     HIPC(c, hipSetDevice(c->device));
     ncclUniqueId u;
     std::copy(id, id + MM_COMM_ID_BYTES, reinterpret_cast<uint8_t*>(u.internal));
@@ -169,6 +201,7 @@ int mm_comm_init_all(int n, mm_ctx* const* ctxs, mm_comm** out) {
             if (devs[j] == devs[i]) return ctx_fail(c0, MM_ERR_INVALID, "mm_comm_init_all: two contexts on one GPU");
         out[i] = nullptr;
     }
+    if (int rc = check_rccl_runtime(c0, "mm_comm_init_all")) return rc;
     std::vector<ncclComm_t> comms(n);
     NCCLC(c0, nullptr, ncclCommInitAll(comms.data(), n, devs.data()));
     for (int i = 0; i < n; ++i) {
@@ -201,6 +234,8 @@ int mm_comm_rccl_version(void) {
     int v = 0;
     return ncclGetVersion(&v) == ncclSuccess ? v : 0;
 }
+
+int mm_comm_rccl_header_version(void) { return NCCL_VERSION_CODE; }
 
 void mm_comm_destroy(mm_comm* m) {
     if (!m) return;
@@ -243,8 +278,10 @@ int mm_gather_rows(mm_ctx* c, mm_comm* m, const void* tile, uint32_t n_frames, u
         if (ge != ncclSuccess) return ctx_fail(c, MM_ERR_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(ge));
     }
     if (m->rank != 0) return MM_OK;
-    return launch_assemble(c, c->d_gather, via ? nullptr : static_cast<const uint8_t*>(tile),
-                           static_cast<uint8_t*>(frame), (uint32_t)m->n, n_frames, rows_max, height, rb);
+    if (int rc = launch_assemble(c, c->d_gather, via ? nullptr : static_cast<const uint8_t*>(tile),
+                                 static_cast<uint8_t*>(frame), (uint32_t)m->n, n_frames, rows_max, height, rb))
+        return rc;
+    return staging_released(c, m->n > 1 || via);
 }
 
 int mm_gather_rows_all(int n, mm_ctx* const* ctxs, mm_comm* const* comms, const void* const* tiles, uint32_t n_frames,
@@ -287,8 +324,10 @@ int mm_gather_rows_all(int n, mm_ctx* const* ctxs, mm_comm* const* comms, const 
         if (ge != ncclSuccess) return ctx_fail(cr, MM_ERR_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(ge));
         HIPC(cr, hipSetDevice(cr->device));
     }
-    return launch_assemble(cr, cr->d_gather, via ? nullptr : static_cast<const uint8_t*>(tiles[root]),
-                           static_cast<uint8_t*>(frame), (uint32_t)n, n_frames, rows_max, height, rb);
+    if (int rc = launch_assemble(cr, cr->d_gather, via ? nullptr : static_cast<const uint8_t*>(tiles[root]),
+                                 static_cast<uint8_t*>(frame), (uint32_t)n, n_frames, rows_max, height, rb))
+        return rc;
+    return staging_released(cr, n > 1 || via);
 }
 
 int mm_assemble_rows(mm_ctx* c, const void* tiles, uint32_t n_ranks, uint32_t n_frames, uint32_t width,

@@ -31,9 +31,6 @@ struct mm_ctx {
     uint2* d_recs = nullptr;    // compact leaf-ordered rect records
     size_t n_fast_recs = 0;
     bool lean_ok = false;       // no SLOW rect records (loop form 7, grid search)
-    float* d_dict_tab = nullptr;       // dictionary-coded nodes (mode 10): 256 values
-    uint32_t* d_dict_words = nullptr;  // 3 words per production node
-    bool dict_ok = false;
     uint8_t* d_grid = nullptr;  // certified grid search (grid_build.cpp, mm_grid.h)
     DevGrid grid{};
     bool grid_ok = false;
@@ -74,10 +71,8 @@ struct mm_ctx {
     int opt_persist = 2;            // 0 one thread per path (k_trace_mega), 2 wave-persistent
     int opt_ww = -1;                // loop form: -1 auto, 0, 5, 7 (BVH), 11 (grid search)
     int opt_lds_rects = 1;          // compact rect records in LDS beside the nodes when they fit
-    uint32_t opt_lds_split = 1;     // top-of-tree LDS cache: 0 off, 1 auto, else KB (always)
     bool opt_fuse = true;           // resolve fused into the wave when 64 % spp == 0
     uint32_t opt_reserve_cus = 0;   // MM_OPT_RESERVE_CUS
-    uint32_t opt_dict = 1;          // MM_OPT_DICT_NODES: 0 off, 1 auto, 2 always (when it fits)
     int opt_defer = -1;             // MM_OPT_DEFER: defer a wave's paths once <= this many lanes run (0 off, -1 auto)
     uint32_t opt_defer_min = 1u << 24;  // MM_OPT_DEFER_MIN: ... in launches of at least this many paths
     int last_form = -1, last_mode = -1;  // of the last wave-persistent launch (mm_scene_info)
@@ -112,6 +107,11 @@ struct mm_ctx {
     // frame-end gather (mm_comm.hip): the root's receive staging, one slab per rank
     uint8_t* d_gather = nullptr;
     size_t gather_cap = 0;
+    // the last gather that used d_gather: its assembly is done at this event (recorded on the stream the gather
+    // ran on); a gather on another stream waits for it before reusing the staging, and a regrow waits before
+    // freeing it (two gathers on different streams raced on the one staging buffer)
+    hipEvent_t gather_done = nullptr;
+    bool gather_pending = false;
 };
 
 namespace mm {

@@ -114,16 +114,10 @@ struct DevScene {
     const float4* shade;      // 2 * n_rects
     const uint32_t* idx;      // n_rects
     uint32_t n_nodes;         // production array length in nodes (breadth-first pairs)
-    uint32_t n_lds_f4;        // float4s of `nodes` staged in LDS by split-cache kernels
     uint32_t n_rects;
     uint32_t root_packed;     // count<<24 | left_first of node 0
     uint32_t fast_ok;         // scene coordinates inside the Markstein guard
     const uint2* recs;        // 5 x uint2 per BVH slot: compact rect records (rect_compact.cpp)
-    // Dictionary-coded nodes (LDS mode 10, MM_OPT_DICT_NODES): the distinct bound
-    // values (<= 256) and 3 words per production node: 8-bit indices of
-    // (mn.x, mx.x, mn.y, mx.y), of (mn.z, mx.z), and the packed child word
-    const float* dict_tab;      // 256 floats
-    const uint32_t* dict_words; // 3 * n_nodes
     DevGrid grid;
 };
 

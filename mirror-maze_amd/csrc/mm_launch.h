@@ -92,12 +92,11 @@ constexpr uint32_t kStatusDone = 0x80000000u;
 hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s);
 
 struct MegaOpts {
-    bool reference = false;   // traverse_reference (IEEE division), A/B baseline
-    bool lds_nodes = false;   // stage nodes in LDS
+    bool reference = false;   // traverse_reference (IEEE division): MM_PIPE_REFERENCE, the only form built
     uint32_t block = 256;     // threads per workgroup
 };
 
-// Throughput mode, megakernel: one thread per (pixel, sample) path; writes
+// MM_PIPE_REFERENCE: one thread per (pixel, sample) path; writes
 // the per-sample value sqrt(max(L,0)) to samples[path] (path = pixel*spp+s).
 hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples,
                              unsigned long long* stats_dev, uint32_t* err, bool count_stats,
@@ -121,9 +120,6 @@ bool wavepersist_built(int lds_mode, int form);
 // Register / scratch / LDS use of the (kStats = false) instance.
 // ring: 0 no tail deferral, 1 rings with global records, 2 rings with records in LDS.
 hipError_t wavepersist_attributes(int lds_mode, int form, int ring, hipFuncAttributes* a);
-// Built with -DMM_AB_VARIANTS (the A/B-only placements and k_trace_mega's
-// non-reference forms).
-bool ab_variants_built();
 // Display stage (display.hip).
 hipError_t launch_present_blur(const uint32_t* in, uint32_t* out, uint32_t W, uint32_t H, hipStream_t s);
 hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32_t n_chunks, uint32_t W, uint32_t H,

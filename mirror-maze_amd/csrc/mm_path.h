@@ -103,6 +103,7 @@ __device__ __forceinline__ F3 trace_path(const DevScene& sc, const Q& query, F3 
     p.L = F3{0.0f, 0.0f, 0.0f};
     p.n = 0;
     p.mh = 0;
+    p.bank = 0u;
     bounce_loop<kStats>(sc, query, p, bounce_limit, mirror_limit, stack, c, overflow);
     return F3{sqrtf(fmaxf(p.L.x, 0.0f)), sqrtf(fmaxf(p.L.y, 0.0f)), sqrtf(fmaxf(p.L.z, 0.0f))};
 }

@@ -16,7 +16,6 @@
 #include <new>
 #include <string>
 #include <thread>
-#include <unordered_set>
 #include <vector>
 
 #include "grid_build.h"
@@ -68,8 +67,6 @@ DevScene dev_scene(const mm_ctx* c) {
     s.geo = c->d_geo;
     s.recs = c->d_recs;
     s.grid = c->grid;
-    s.dict_tab = c->d_dict_tab;
-    s.dict_words = c->d_dict_words;
     s.shade = c->d_shade;
     s.idx = c->d_idx;
     s.n_nodes = c->n_nodes;
@@ -83,8 +80,6 @@ void free_scene(mm_ctx* c) {
     (void)hipFree(c->d_grid);
     c->d_grid = nullptr; c->grid = DevGrid{}; c->grid_ok = false; c->grid_slow = false; c->grid_wide = false;
     c->grid_flat = false;
-    (void)hipFree(c->d_dict_tab); (void)hipFree(c->d_dict_words);
-    c->d_dict_tab = nullptr; c->d_dict_words = nullptr; c->dict_ok = false;
     c->d_rects = nullptr; c->d_nodes = nullptr; c->d_nodes_ref = nullptr; c->d_geo = nullptr; c->d_recs = nullptr; c->d_shade = nullptr; c->d_idx = nullptr;
     c->has_scene = false;
 }
@@ -297,7 +292,7 @@ int report_failure(mm_ctx* c, const char* suffix) {
 extern "C" {
 
 const char* mm_version(void) {
-    return ab_variants_built() ? "mirror-maze-amd 0.3 gfx950+ab" : "mirror-maze-amd 0.3 gfx950";
+    return "mirror-maze-amd 0.4 gfx950";
 }
 
 int mm_create(int device, mm_ctx** out) {
@@ -349,6 +344,7 @@ void mm_destroy(mm_ctx* c) {
     (void)hipFree(c->d_fb8_alt); (void)hipFree(c->d_packets);
     (void)hipFree(c->d_samples); (void)hipFree(c->d_aux); (void)hipFree(c->d_tail); (void)hipFree(c->d_work);
     (void)hipFree(c->d_gather);
+    if (c->gather_done) (void)hipEventDestroy(c->gather_done);
     if (c->h_status) (void)hipHostFree(c->h_status);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -385,8 +381,11 @@ int mm_set_pipeline(mm_ctx* c, int pipe) {
     return MM_OK;
 }
 
-static const char* const kAbOnly =
-    "this A/B-only kernel variant is built only with `make EXTRA=-DMM_AB_VARIANTS` (DESIGN.md §4)";
+// Kernel variants removed in round 6: every one measured slower than what
+// MM_PIPE_AUTO selects; the options that chose them are refused by name.
+static const char* const kRemoved =
+    "this kernel variant (one thread per path over the production BVH forms, loop form 0, the split node "
+    "cache, dictionary-coded nodes) measured slower and was removed (DESIGN.md §4)";
 
 int mm_set_option(mm_ctx* c, int key, int value) {
     if (!c) return MM_ERR_INVALID;
@@ -398,21 +397,20 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_PERSIST:
             if (value != 0 && value != 2) return fail(c, MM_ERR_INVALID, "persist must be 0 or 2");
-            if (value == 0 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
+            if (value == 0) return fail(c, MM_ERR_UNSUPPORTED, kRemoved);
             c->opt_persist = value;
             return MM_OK;
         case MM_OPT_TRAVERSAL:
             if (value != -1 && value != 0 && value != 5 && value != 7 && value != 11)
                 return fail(c, MM_ERR_INVALID, "traversal must be -1 (auto), 0, 5, 7 or 11 (grid search)");
-            if (value == 0 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
+            if (value == 0) return fail(c, MM_ERR_UNSUPPORTED, kRemoved);
             c->opt_ww = value;
             return MM_OK;
         case MM_OPT_LDS_RECTS: c->opt_lds_rects = value != 0; return MM_OK;
         case MM_OPT_LDS_SPLIT:
             if (value < 0) return fail(c, MM_ERR_INVALID, "split cache size must be >= 0 (0 off, 1 auto, else KB)");
-            if (value > 1 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
-            c->opt_lds_split = (uint32_t)value;
-            return MM_OK;
+            if (value > 1) return fail(c, MM_ERR_UNSUPPORTED, kRemoved);
+            return MM_OK;  // 0 / 1: accepted, nothing to select (no split cache is built)
         case MM_OPT_FUSE_RESOLVE: c->opt_fuse = value != 0; return MM_OK;
         case MM_OPT_RESERVE_CUS:
             if (value < 0 || value > 128) return fail(c, MM_ERR_INVALID, "reserved CUs must be 0..128");
@@ -428,9 +426,8 @@ int mm_set_option(mm_ctx* c, int key, int value) {
             return MM_OK;
         case MM_OPT_DICT_NODES:
             if (value < 0 || value > 2) return fail(c, MM_ERR_INVALID, "dict nodes must be 0, 1 or 2");
-            if (value == 2 && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
-            c->opt_dict = (uint32_t)value;
-            return MM_OK;
+            if (value == 2) return fail(c, MM_ERR_UNSUPPORTED, kRemoved);
+            return MM_OK;  // 0 / 1: accepted, nothing to select (no dictionary is built)
         case MM_OPT_GRID_MERGE: c->opt_grid_merge = value != 0; return MM_OK;
         case MM_OPT_GRID_WIDE: c->opt_grid_wide = value != 0; return MM_OK;
         case MM_OPT_GRID_CELL:
@@ -459,11 +456,12 @@ int mm_scene_info(const mm_ctx* c, int key, double* value) {
         case MM_INFO_GRID_INDEX_BYTES: *value = g.off_data; return MM_OK;
         case MM_INFO_LEAN: *value = c->lean_ok ? 1.0 : 0.0; return MM_OK;
         case MM_INFO_DEPTH: *value = c->depth; return MM_OK;
-        case MM_INFO_DICT_OK: *value = c->dict_ok ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_DICT_OK: *value = 0.0; return MM_OK;  // (dictionary-coded nodes removed in round 6)
         case MM_INFO_LAST_FORM: *value = c->last_form; return MM_OK;
         case MM_INFO_LAST_LDS_MODE: *value = c->last_mode; return MM_OK;
         case MM_INFO_GRID_FACES: *value = c->grid_ok && c->grid_wide ? 1.0 : 0.0; return MM_OK;
         case MM_INFO_LAST_DEFER: *value = c->last_defer ? 1.0 : 0.0; return MM_OK;
+        case MM_INFO_GRID_LDS_CAP: *value = wavepersist_grid_cap(0); return MM_OK;
         case MM_INFO_LAST_VGPRS:
         case MM_INFO_LAST_SCRATCH:
         case MM_INFO_LAST_STATIC_LDS: {
@@ -525,42 +523,6 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
             packed[2 * i] = make_float4(nd.mn[0], nd.mx[0], nd.mn[1], nd.mx[1]);
             packed[2 * i + 1] = make_float4(nd.mn[2], nd.mx[2], pkf, 0.0f);
         }
-    // Dictionary-coded nodes (mode 10): the distinct bound values of the
-    // production array, 8-bit indices when there are at most 256.  Skipped
-    // with MM_OPT_DICT_NODES 0; the scan stops at the 257th distinct value.
-    auto fbits = [](float x) { uint32_t b; std::memcpy(&b, &x, 4); return b; };
-    std::vector<float> dict;
-    bool dict_ok = c->opt_dict != 0;
-    if (dict_ok) {
-        std::unordered_set<uint32_t> seen;
-        auto add = [&](float x) {
-            if (seen.insert(fbits(x)).second) {
-                dict.push_back(x);
-                if (dict.size() > 256) dict_ok = false;
-            }
-        };
-        for (size_t i = 0; i < packed.size() && dict_ok; i += 2) {
-            add(packed[i].x); add(packed[i].y); add(packed[i].z); add(packed[i].w);
-            add(packed[i + 1].x); add(packed[i + 1].y);
-        }
-    }
-    std::vector<uint32_t> dict_words;
-    if (dict_ok) {
-        std::sort(dict.begin(), dict.end(), [&](float a, float b) { return fbits(a) < fbits(b); });
-        auto code = [&](float x) {
-            const uint32_t b = fbits(x);
-            return (uint32_t)(std::lower_bound(dict.begin(), dict.end(), x,
-                                               [&](float a, float) { return fbits(a) < b; }) - dict.begin());
-        };
-        dict_words.resize(3 * (size_t)n_prod);
-        for (uint32_t i = 0; i < n_prod; ++i) {
-            const float4 a = packed[2 * (size_t)i], b = packed[2 * (size_t)i + 1];
-            dict_words[3 * (size_t)i] = code(a.x) | code(a.y) << 8 | code(a.z) << 16 | code(a.w) << 24;
-            dict_words[3 * (size_t)i + 1] = code(b.x) | code(b.y) << 8;
-            dict_words[3 * (size_t)i + 2] = fbits(b.z);
-        }
-        dict.resize(256, 0.0f);
-    }
     bool fast = true;
     for (uint32_t i = 0; i < n_nodes && fast; ++i)
         for (int a = 0; a < 3; ++a) fast = fast && coord_ok(nodes[i].mn[a]) && coord_ok(nodes[i].mx[a]);
@@ -593,8 +555,10 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     // certified grid search (mm_grid.h): needs the Markstein guards and axis-aligned rects
     GridHost gh;
     std::string gwhy;
-    // (80 KB: the LDS of one of the two 1024-thread blocks per CU)
-    const bool grid_ok = fast && build_grid(rects, n_rects, nodes, n_nodes, idx, 80 * 1024, gh, gwhy,
+    // the budget: what the static grid array of modes 11 / 14 holds beside the kernel's other static LDS
+    // (wavepersist_grid_cap(0), 80 KB -- the LDS of one of the two 1024-thread blocks per CU -- less its
+    // claimed-range words; ADVICE r05: an image between that and 80 KB failed the launch)
+    const bool grid_ok = fast && build_grid(rects, n_rects, nodes, n_nodes, idx, wavepersist_grid_cap(0), gh, gwhy,
                                             c->opt_grid_merge, c->opt_grid_cell / 100.0, c->opt_grid_wide);
     if (!fast) gwhy = "scene coordinates outside the exact-division guards";
     DevGrid dg{};
@@ -625,13 +589,6 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         c->grid_flat = gh.flat_ok;
     }
     HIPC(c, hipMemcpyAsync(c->d_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-    if (dict_ok) {
-        HIPC(c, hipMalloc((void**)&c->d_dict_tab, 256 * sizeof(float)));
-        HIPC(c, hipMalloc((void**)&c->d_dict_words, dict_words.size() * sizeof(uint32_t)));
-        HIPC(c, hipMemcpyAsync(c->d_dict_tab, dict.data(), 256 * sizeof(float), hipMemcpyHostToDevice, c->stream));
-        HIPC(c, hipMemcpyAsync(c->d_dict_words, dict_words.data(), dict_words.size() * sizeof(uint32_t),
-                               hipMemcpyHostToDevice, c->stream));
-    }
     HIPC(c, hipMemcpyAsync(c->d_idx, idx, n_rects * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPC(c, launch_prep_rects(c->d_rects, n_rects, c->d_geo, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));  // host arrays may be freed on return
@@ -644,7 +601,6 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
     c->grid = dg;
     c->grid_ok = grid_ok;
     c->grid_why = grid_ok ? std::string() : gwhy;
-    c->dict_ok = dict_ok;
     c->has_scene = true;
     return MM_OK;
 }
@@ -749,12 +705,8 @@ namespace {
 // 1024-thread blocks at 8 waves per SIMD -> two blocks per CU -> 80 KB of LDS
 // each.  Auto (MM_OPT_TRAVERSAL -1): the certified grid search when the scene
 // allows it (C3 ...), else the lean BVH loop (form 7) when every rect has a
-// compact record, else form 5.  BVH data placement: nodes + records in LDS
-// when both fit; nodes in LDS, records through L1/L2 when only the nodes do;
-// otherwise dictionary-coded nodes (mode 10) when they fit, else the top of
-// the tree (split cache, mode 6).  An explicit MM_OPT_LDS_SPLIT > 1 always
-// uses the split cache of that size; MM_OPT_DICT_NODES 2 always uses the
-// dictionary when it fits; MM_OPT_LDS_NODES 0 stages nothing.
+// compact record and the nodes + records fit LDS, else form 5 with the nodes
+// in LDS when they fit, else through L1/L2.  MM_OPT_LDS_NODES 0 stages nothing.
 int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
     const size_t budget = 80 * 1024;
     const bool auto_form = c->opt_ww < 0;
@@ -776,13 +728,15 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
             mode = m;
             return MM_OK;
         };
-        if (c->grid_wide) {  // built only when the whole image fits the LDS budget (grid_build.cpp)
+        // modes 11 / 14 stage into the kernel's static grid array: their images must fit its capacity
+        const size_t cap = wavepersist_grid_cap(0);
+        if (c->grid_wide) {  // built only when the whole image fits that capacity (grid_build.cpp)
             form += kFormGridWide - kFormGrid;
-            return flat(c->opt_lds ? 11 : 13);
+            return flat(c->opt_lds && c->grid.bytes <= cap ? 11 : 13);
         }
-        if (c->opt_lds && c->grid.bytes <= budget) return flat(11);
+        if (c->opt_lds && c->grid.bytes <= cap) return flat(11);
         // compact records + class table + index (N=64: ~77 KB), leaf boxes global
-        if (c->opt_lds && c->grid_flat && c->grid.off_box <= budget) return flat(14);
+        if (c->opt_lds && c->grid_flat && c->grid.off_box <= cap) return flat(14);
         if (c->opt_lds && c->grid.off_data <= budget) return flat(12);
         if (!auto_form || !c->opt_lds) return flat(13);
         // the index does not fit LDS: auto takes the BVH (nodes in LDS or cached), which is not
@@ -795,44 +749,17 @@ int choose_wavepersist(mm_ctx* c, DevScene& sc, int& form, int& mode) {
     }
     const size_t nodes_b = 2 * (size_t)c->n_nodes * sizeof(float4);
     const size_t recs_b = 40 * (size_t)c->n_rects;
-    const size_t dict_b = 256 * sizeof(float) + 12 * (size_t)c->n_nodes;
-    const bool dict_fits = c->opt_dict && c->dict_ok && dict_b <= budget;
-    if (!ab_variants_built()) {
-        // default build: nodes + records in LDS (lean form 7 or form 5), nodes only (form 5), or nothing
-        if (c->opt_lds && c->opt_lds_rects && nodes_b + recs_b <= budget) {
-            mode = 3;
-        } else {
-            if (form == kFormLean && !auto_form)
-                return fail(c, MM_ERR_UNSUPPORTED,
-                            std::string("loop form 7 without nodes + records in LDS: ") + kAbOnly);
-            form = kFormLeafInterior;
-            mode = (c->opt_lds && nodes_b <= budget) ? 1 : 0;
-        }
-        return MM_OK;
-    }
-    if (!c->opt_lds) {
-        mode = 0;
-    } else if (c->opt_dict == 2 && dict_fits) {
-        mode = 10;
-    } else if (c->opt_lds_split > 1) {
-        mode = 6;
-        sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, (size_t)c->opt_lds_split * 1024 /
-                                                                              sizeof(float4)) & ~3u;
-    } else if (nodes_b <= budget) {
-        mode = (c->opt_lds_rects && nodes_b + recs_b <= budget) ? 3 : (form == kFormIfIf ? 1 : 7);
-    } else if (dict_fits) {
-        mode = 10;
-    } else if (c->opt_lds_split == 1) {
-        mode = 6;
-        sc.n_lds_f4 = (uint32_t)std::min<size_t>(2 * (size_t)c->n_nodes, budget / sizeof(float4)) & ~3u;
+    // nodes + records in LDS (lean form 7 or form 5), nodes only (form 5), or nothing
+    if (c->opt_lds && c->opt_lds_rects && nodes_b + recs_b <= budget) {
+        mode = 3;
     } else {
-        mode = 0;
+        if (form == kFormLean && !auto_form)
+            return fail(c, MM_ERR_UNSUPPORTED,
+                        "loop form 7 needs the BVH nodes + compact records in LDS (its other placements "
+                        "measured slower and were removed, DESIGN.md §4)");
+        form = kFormLeafInterior;
+        mode = (c->opt_lds && nodes_b <= budget) ? 1 : 0;
     }
-    if (form == kFormLean && mode == 0) form = kFormLeafInterior;
-    // the lean form with the split cache measured slower (C5 scene 30.6 vs 29.4 ms): auto keeps form 5 there
-    if (auto_form && form == kFormLean && mode == 6) form = kFormLeafInterior;
-    if (form == kFormIfIf && mode != 1 && mode != 3)
-        return fail(c, MM_ERR_UNSUPPORTED, "loop form 0 is built for nodes in LDS only (LDS modes 1, 3)");
     return MM_OK;
 }
 
@@ -859,7 +786,10 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     if (rgba8 && (e->flags & MM_EXT_ACCUMULATE))
         return fail(c, MM_ERR_INVALID, "mm_trace_tile: MM_EXT_RGBA8 frames cannot accumulate");
     const size_t out_bpp = rgba8 ? 4 : 16;
-    if (reinterpret_cast<uintptr_t>(out_dev) % 4) return fail(c, MM_ERR_INVALID, "mm_trace_tile: misaligned output");
+    // the stores are out_bpp wide (a float4 per pixel, or one RGBA8 word): the output must be aligned to that
+    if (reinterpret_cast<uintptr_t>(out_dev) % out_bpp)
+        return fail(c, MM_ERR_INVALID, std::string("mm_trace_tile: output not ") + std::to_string(out_bpp) +
+                                           "-byte aligned");
     HIPC(c, hipSetDevice(c->device));
     const bool want_stats = (e->flags & MM_EXT_COUNT_STATS) != 0;
     const uint64_t row_paths = (uint64_t)w * e->spp;
@@ -867,7 +797,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
     // MM_PIPE_WAVEFRONT: the wave-persistent kernel with mirror-tail deferral (compaction) always on
     const bool wave = c->pipe == MM_PIPE_WAVEFRONT;
     const bool persist = c->pipe != MM_PIPE_REFERENCE && (wave || c->opt_persist == 2);
-    if (!persist && c->pipe != MM_PIPE_REFERENCE && !ab_variants_built()) return fail(c, MM_ERR_UNSUPPORTED, kAbOnly);
+    if (!persist && c->pipe != MM_PIPE_REFERENCE) return fail(c, MM_ERR_UNSUPPORTED, kRemoved);
     int form = 0, mode = 0;
     DevScene sc = dev_scene(c);
     if (persist) {
@@ -990,7 +920,6 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         rc = [&]() -> int {
             if (int r = prof_mark(c)) return r;
             if (c->opt_fault == 3) return fail(c, MM_ERR_HIP, "injected enqueue failure (MM_OPT_FAULT_INJECT 3)");
-            const bool lds_fits = c->opt_lds && 2 * (size_t)c->n_nodes * sizeof(float4) <= 64 * 1024;
             if (persist) {
                 c->last_form = form >= kFormGrid ? kFormGrid : form;
                 c->last_mode = mode;
@@ -1003,8 +932,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
             } else {
                 MegaOpts mo;
                 mo.reference = c->pipe == MM_PIPE_REFERENCE;
-                mo.lds_nodes = lds_fits;
-                mo.block = c->opt_block ? c->opt_block : (mo.lds_nodes ? 512u : 256u);
+                mo.block = c->opt_block ? c->opt_block : 256u;
                 HIPC(c, launch_trace_mega(dev_scene(c), job, c->d_samples, c->d_aux, err_dev, want_stats, mo,
                                           c->stream));
                 enqueued = true;  // the kernel runs: its slot is written by the publish below or here

@@ -202,47 +202,11 @@ template <typename N, typename R> __device__ __forceinline__ CompactView<N, R> v
     return CompactView<N, R>{n, r};
 }
 
-// Top-of-tree cache for scenes whose nodes exceed the LDS budget: production
-// float4s [0, n_lds) are staged in LDS, the rest are read from global memory.
-// Child pairs are numbered breadth-first at upload (mm_runtime.hip), so the
-// LDS part holds the top levels every traversal visits.
-struct SplitNodes {
-    const float4* lds;
-    const float4* glob;
-    uint32_t n_lds;
-};
-
 // The two children of an interior node: one adjacent 64-B pair at 2*lf.
 __device__ __forceinline__ void node_pair(const float4* n, uint32_t lf, float4& la, float4& lb, float4& ra,
                                           float4& rb) {
     la = n[2 * lf]; lb = n[2 * lf + 1]; ra = n[2 * lf + 2]; rb = n[2 * lf + 3];
 }
-__device__ __forceinline__ void node_pair(const SplitNodes& n, uint32_t lf, float4& la, float4& lb, float4& ra,
-                                          float4& rb) {
-    if (2 * lf < n.n_lds) node_pair(n.lds, lf, la, lb, ra, rb);
-    else node_pair(n.glob, lf, la, lb, ra, rb);
-}
-
-// Dictionary-coded nodes in LDS (mode 10): 12 B per node, so the N=64 tree
-// (5534 nodes, 66 KB + a 1 KB value table) fits the LDS budget.  Decoding
-// returns the production layout's values exactly (the table holds the
-// original floats).  Left children sit at even production indices, so a pair
-// (24 B at 12 * lf) is 8-B aligned.
-struct DictNodes {
-    const uint32_t* w;   // 3 words per node
-    const float* tab;    // 256 bound values
-};
-__device__ __forceinline__ void node_pair(const DictNodes& n, uint32_t lf, float4& la, float4& lb, float4& ra,
-                                          float4& rb) {
-    const uint2* p = reinterpret_cast<const uint2*>(n.w + 3 * lf);
-    const uint2 q0 = p[0], q1 = p[1], q2 = p[2];
-    // left child: q0.x (4 indices), q0.y (2 indices), q1.x packed; right: q1.y, q2.x, q2.y
-    la = make_float4(n.tab[q0.x & 255u], n.tab[(q0.x >> 8) & 255u], n.tab[(q0.x >> 16) & 255u], n.tab[q0.x >> 24]);
-    lb = make_float4(n.tab[q0.y & 255u], n.tab[(q0.y >> 8) & 255u], __uint_as_float(q1.x), 0.0f);
-    ra = make_float4(n.tab[q1.y & 255u], n.tab[(q1.y >> 8) & 255u], n.tab[(q1.y >> 16) & 255u], n.tab[q1.y >> 24]);
-    rb = make_float4(n.tab[q2.x & 255u], n.tab[(q2.x >> 8) & 255u], __uint_as_float(q2.y), 0.0f);
-}
-
 __device__ __forceinline__ float sel3(uint32_t a, F3 v) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
 
 // ray_rect_intersect on a compact record (FAST kind) for a fast-guarded ray;
@@ -489,12 +453,30 @@ __device__ __forceinline__ bool closest_hit_bvh(const DevScene& sc, const V& v, 
     }
 }
 
-// Path state carried across bounces.
+// Path state carried across bounces.  bank = 1: the rejection-sampling trial
+// last drawn from the RNG (its three numbers end at `seed`) was accepted and
+// is the direction sample of the path's next diffuse bounce (shade_step).
 struct PathState {
     F3 ori, dir, T, L;
     uint32_t seed;
     int n, mh;
+    uint32_t bank;
 };
+
+// random()'s state step s -> a s + c (shaders.metal:181-186, rand_pm1), and the
+// inverse of three steps: s0 = A s3 + C with A = a^-3, C = -A c (1 + a + a^2)
+// mod 2^32 (a is odd, so invertible), rewinding one trial's three draws.
+constexpr uint32_t kLcgA = 747796405u, kLcgC = 291336453u;
+constexpr uint32_t lcg_inv(uint32_t a) {  // Newton's iteration for the inverse of an odd a mod 2^32
+    uint32_t x = a;
+    for (int i = 0; i < 5; ++i) x *= 2u - a * x;
+    return x;
+}
+constexpr uint32_t kLcgBack3A = lcg_inv(kLcgA * kLcgA * kLcgA);
+constexpr uint32_t kLcgBack3C = 0u - kLcgBack3A * (kLcgC * (1u + kLcgA + kLcgA * kLcgA));
+static_assert(kLcgA * kLcgA * kLcgA * kLcgBack3A == 1u, "a^3 * a^-3 = 1 mod 2^32");
+static_assert(kLcgBack3A * (((kLcgA * 12345u + kLcgC) * kLcgA + kLcgC) * kLcgA + kLcgC) + kLcgBack3C == 12345u,
+              "three steps rewound");
 
 // One shading step after a closest-hit query (the body of shaders.metal:306-340
 // after line 307).  Returns false when the path terminates.
@@ -516,21 +498,47 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         const float4 e = sc.shade[2 * k + 1];
         contrib = (e.w * p.T) * xyz(e);                      // %253, %254
         p.T = xyz(s0) * p.T;                                 // %264
-        float rx = rand_pm1(p.seed), ry = rand_pm1(p.seed), rz = rand_pm1(p.seed);
+        // shaders.metal:316-318, length(r) > 1: RN(sqrt(x)) > 1 <=> x > 1 + 2^-23
+        // for every binary32 x (exhaustive check: scripts/verify_sqrt_gt1.c).
+        // The path's direction samples are its RNG stream's accepted trials in
+        // order -- nothing else draws from it after the primary jitter -- so a
+        // lane may draw ahead.  The first trial: the banked one (its draws
+        // rewound and redrawn: the same numbers, the state ends where it was),
+        // else a fresh one.  Lanes whose trial is rejected loop; while they do,
+        // the wave's other diffuse lanes draw their NEXT bounce's trials until
+        // one is accepted (the bank), so that bounce's first trial is accepted
+        // on those lanes and the wave's loop runs for fewer lanes -- a wave runs
+        // its unluckiest lane's trials (~5.8 iterations per bounce on C3 where a
+        // lane needs 0.9).  (A wave-pooled form -- trials spread over the lanes
+        // with jumps of the state -- was bit-exact and slower: 12 % on C3 in
+        // round 2, 3.5 % in round 3, profiles/r03/ab_pool_trials.txt.)
+        uint32_t s = p.seed;
+        if (p.bank) s = s * kLcgBack3A + kLcgBack3C;
+        float rx = rand_pm1(s), ry = rand_pm1(s), rz = rand_pm1(s);
+        p.seed = s;
         F3 rd = F3{rx, ry, rz};
         float len2 = dot3(rd, rd);
-        // shaders.metal:316-318, length(r) > 1: RN(sqrt(x)) > 1 <=> x > 1 + 2^-23
-        // for every binary32 x (exhaustive check: scripts/verify_sqrt_gt1.c)
-        // (a wave-pooled form of this loop -- the unluckiest lanes' trials spread
-        // over the others with jumps of the random() state -- was bit-exact and
-        // slower: 12 % on C3 in round 2, 3.5 % in round 3 with LDS state
-        // broadcast + ds_bpermute results, profiles/r03/ab_pool_trials.txt)
-        while (len2 > 0x1.000002p0f) {
+        uint32_t need = len2 > 0x1.000002p0f ? 1u : 0u, bank = 0u;
+        if (__builtin_amdgcn_ballot_w64(need != 0u)) do {  // (do-while: no copies of the carried values)
             MM_LANE_STAT(kLpTrial);
-            rx = rand_pm1(p.seed); ry = rand_pm1(p.seed); rz = rand_pm1(p.seed);
-            rd = F3{rx, ry, rz};
-            len2 = dot3(rd, rd);
-        }
+            // every lane draws (no branch: the loop is one block); a lane already
+            // holding a banked trial keeps its state (need = 1 implies bank = 0)
+            uint32_t t = p.seed;
+            rx = rand_pm1(t); ry = rand_pm1(t); rz = rand_pm1(t);
+            const float q2 = dot3(F3{rx, ry, rz}, F3{rx, ry, rz});
+            // accepted <=> !(q2 > 1 + 2^-23) <=> q2 < 1 + 2^-22 <=> the sign of the exact difference
+            // (q2 is finite) -- two pairable ops instead of a compare and a select
+            const uint32_t acc = __float_as_uint(q2 - 0x1.000004p0f) >> 31;
+            p.seed = bank ? p.seed : t;
+            const uint32_t take = need & acc;
+            rd.x = take ? rx : rd.x;
+            rd.y = take ? ry : rd.y;
+            rd.z = take ? rz : rd.z;
+            len2 = take ? q2 : len2;
+            bank |= acc - take;  // accepted on a lane that did not need it
+            need -= take;
+        } while (__builtin_amdgcn_ballot_w64(need != 0u));
+        p.bank = bank;
         const F3 rn = rsq(len2) * rd;                        // %358
         x = rn + side * nn;                                  // %367
     } else {

@@ -2,8 +2,8 @@
 //
 //   k_prep_rects         per-rect subexpressions of ray_rect_intersect
 //   k_trace_chunks       parity mode: the reference dispatch (shaders.metal:245-368)
-//   k_trace_mega         throughput mode, one thread per (pixel, sample) path
-//                        (and MM_PIPE_REFERENCE, the straight statement)
+//   k_trace_mega         MM_PIPE_REFERENCE: one thread per (pixel, sample) path,
+//                        the straight statement (IEEE division everywhere)
 //   k_trace_wavepersist  throughput mode, the production kernel: resident
 //                        blocks, waves pull 64-path chunks, pixels resolved in
 //                        the wave
@@ -99,9 +99,11 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
 }
 
 // ---------------------------------------------------------------------------
-// Throughput mode, one thread per path: path = pixel*spp + sample.
-//   kRef  : traverse_reference (IEEE division everywhere), for A/B
-//   kLds  : stage the node array in LDS (dynamic shared memory) first
+// MM_PIPE_REFERENCE, one thread per path: path = pixel*spp + sample, the
+// straight statement of the reference walk (traverse_reference, IEEE division
+// everywhere).  (The round-1 one-thread-per-path kernels over the production
+// BVH loop forms measured slower than the wave-persistent kernel and were
+// removed in round 6)
 template <bool kStats, typename Q>
 __device__ __forceinline__ void mega_body(const DevScene& sc, const Q& q, const TileJob& job,
                                           float4* __restrict__ samples, unsigned long long* stats, uint32_t* err) {
@@ -126,21 +128,10 @@ __device__ __forceinline__ void mega_body(const DevScene& sc, const Q& q, const 
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
 }
 
-template <bool kStats, bool kRef, bool kLds>
+template <bool kStats>
 __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
                                                      unsigned long long* stats, uint32_t* err) {
-    if constexpr (kRef) {
-        mega_body<kStats>(sc, RefQuery<kStats>{sc}, job, samples, stats, err);
-    } else if constexpr (kLds) {
-        extern __shared__ float4 lds_nodes[];
-        for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds_nodes[i] = sc.nodes[i];
-        __syncthreads();
-        mega_body<kStats>(sc, BvhQuery<kStats, kFormIfIf, NodeView<float4*>>{sc, view(lds_nodes)}, job, samples,
-                          stats, err);
-    } else {
-        mega_body<kStats>(sc, BvhQuery<kStats, kFormIfIf, NodeView<const float4*>>{sc, view(sc.nodes)}, job,
-                          samples, stats, err);
-    }
+    mega_body<kStats>(sc, RefQuery<kStats>{sc}, job, samples, stats, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -163,7 +154,7 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // resolve).
 
 // A deferred path's state (64 B: ori.xyz dir.x | dir.yz T.xy | T.z L.xyz |
-// seed, n | mh << 16, sample slot, 0) into / out of slot s of its block's tail
+// seed, n | mh << 16, sample slot, bank) into / out of slot s of its block's tail
 // ring.  kLdsPay (the deferral kernel with kRing = 2, chosen where the grid
 // image leaves room -- C3: 44 KB image + 34 KB static LDS per block, two
 // blocks per CU): the payload lives in the block's LDS beside the turn words,
@@ -184,7 +175,7 @@ __device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t s, const
                                 __float_as_uint(p.T.y));
     const uint4 w2 = make_uint4(__float_as_uint(p.T.z), __float_as_uint(p.L.x), __float_as_uint(p.L.y),
                                 __float_as_uint(p.L.z));
-    const uint4 w3 = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, 0u);
+    const uint4 w3 = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, p.bank);
     if constexpr (kLdsPay) {
         uint4* r = ring_pay() + s;
         r[0] = w0; r[kTailRing] = w1; r[2 * kTailRing] = w2; r[3 * kTailRing] = w3;
@@ -211,6 +202,7 @@ __device__ __forceinline__ uint32_t tail_load(const TailQueue& q, uint32_t s, Pa
     p.seed = d.x;
     p.n = (int)(d.y & 0xFFFFu);
     p.mh = (int)(d.y >> 16);
+    p.bank = d.w;
     return d.z;
 }
 
@@ -499,6 +491,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             p.L = F3{0.0f, 0.0f, 0.0f};
             p.n = 0;
             p.mh = 0;
+            p.bank = 0u;
             bool overflow = false;
             bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow);
             if (overflow) atomicOr(err, kErrStack);
@@ -679,12 +672,9 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
 
 // LDS modes (what a resident block stages before tracing; the rest is read
 // through L1/L2):
-//   0  nothing (nodes, records global)           BVH forms 5
-//   1  BVH nodes                                  BVH forms 0 / 5 (general rect test)
-//   3  BVH nodes + compact slot records           BVH forms 0 / 5 / 7
-//   6  top of the breadth-first node array        BVH forms 5 / 7 (split cache)
-//   7  BVH nodes, compact records global          BVH forms 5 / 7
-//   10 dictionary-coded nodes, records global     BVH forms 5 / 7
+//   0  nothing (nodes, records global)           BVH form 5
+//   1  BVH nodes                                  BVH form 5 (general rect test)
+//   3  BVH nodes + compact slot records           BVH forms 5 / 7
 //   11 the whole grid image                       grid search
 //   12 grid cells + lists, records + boxes global grid search
 //   13 nothing (the grid image global)             grid search
@@ -776,22 +766,7 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         const auto gv = grid_view(GlobalCells{reinterpret_cast<const char*>(sc.grid.cells)}, GlobalList{sc.grid.list},
                                   sc.grid.recs, sc.grid.box, sc.grid.cls);
         return body(GridQuery<kStats, grid_slow(kForm), grid_wide(kForm), grid_flat(kForm), decltype(gv)>{sc, gv});
-    } else if constexpr (kLds == 6) {
-        for (uint32_t i = threadIdx.x; i < sc.n_lds_f4; i += blockDim.x) lds[i] = sc.nodes[i];
-        __syncthreads();
-        staged();
-        const auto v = view(SplitNodes{lds, sc.nodes, sc.n_lds_f4}, sc.recs);
-        return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
-    } else if constexpr (kLds == 10) {
-        float* tab = reinterpret_cast<float*>(lds);
-        uint32_t* words = reinterpret_cast<uint32_t*>(tab + 256);
-        for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = sc.dict_tab[i];
-        for (uint32_t i = threadIdx.x; i < 3 * sc.n_nodes; i += blockDim.x) words[i] = sc.dict_words[i];
-        __syncthreads();
-        staged();
-        const auto v = view(DictNodes{words, tab}, sc.recs);
-        return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
-    } else if constexpr (kLds == 1 || kLds == 3 || kLds == 7) {
+    } else if constexpr (kLds == 1 || kLds == 3) {
         for (uint32_t i = threadIdx.x; i < 2 * sc.n_nodes; i += blockDim.x) lds[i] = sc.nodes[i];
         uint2* lds_recs = reinterpret_cast<uint2*>(lds + 2 * sc.n_nodes);
         if constexpr (kLds == 3)
@@ -800,9 +775,6 @@ __device__ __forceinline__ uint32_t stage_and_run(const DevScene& sc, const Tile
         staged();
         if constexpr (kLds == 3) {
             const auto v = view(static_cast<float4*>(lds), lds_recs);
-            return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
-        } else if constexpr (kLds == 7) {
-            const auto v = view(static_cast<float4*>(lds), sc.recs);
             return body(BvhQuery<kStats, kForm, decltype(v)>{sc, v});
         } else {
             const auto v = view(static_cast<float4*>(lds));
@@ -947,9 +919,7 @@ size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode) {
         case 11: return sc.grid.bytes;
         case 12: return sc.grid.off_data;
         case 14: return sc.grid.off_box;
-        case 6: return (size_t)sc.n_lds_f4 * sizeof(float4);
-        case 10: return 256 * sizeof(float) + 3 * (size_t)sc.n_nodes * sizeof(uint32_t);
-        case 1: case 7: return 2 * (size_t)sc.n_nodes * sizeof(float4);
+        case 1: return 2 * (size_t)sc.n_nodes * sizeof(float4);
         case 3: return 2 * (size_t)sc.n_nodes * sizeof(float4) + 5 * (size_t)sc.n_rects * sizeof(uint2);
         default: return 0;
     }
@@ -988,16 +958,15 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
 }
 
 // (LDS mode, form) pairs; the tail-deferral variant (MM_OPT_DEFER) is built
-// for the grid search and the lean BVH form with records in LDS.  The
-// default build holds what MM_PIPE_AUTO can select (the grid search, and the
-// BVH forms for scenes the grid cannot take: nodes + records in LDS, nodes
-// only, nothing); the A/B-only placements -- split node cache (6), nodes
-// with global records (7), dictionary nodes (10), loop form 0 -- and the
-// one-thread-per-path kernel are built with `make EXTRA=-DMM_AB_VARIANTS`
-// (mm_version() then ends in "+ab"; every one measured slower).
-// The maze forms (flat grid walk, compact records; grid_build.cpp decides)
-// in every grid placement: a maze grid's compact records are read by no other
-// form.  (No SLOW records in maze grids: no slow maze forms.)
+// for the grid search and the lean BVH form with records in LDS.  The build
+// holds what MM_PIPE_AUTO can select: the grid search, and the BVH forms for
+// scenes the grid cannot take (nodes + records in LDS, nodes only, nothing).
+// (The A/B-only placements -- split node cache, nodes with global records,
+// dictionary nodes, loop form 0 -- measured slower and were removed in round
+// 6)  The maze forms (flat grid walk,
+// compact records; grid_build.cpp decides) in every grid placement: a maze
+// grid's compact records are read by no other form.  (No SLOW records in
+// maze grids: no slow maze forms.)
 #define MM_FLAT_INSTANCES(X)                                                                                  \
     X(11, kFormGridWide + kFormGridFlat) X(11, kFormGrid + kFormGridFlat) X(14, kFormGrid + kFormGridFlat)     \
     X(12, kFormGrid + kFormGridFlat) X(13, kFormGridWide + kFormGridFlat) X(13, kFormGrid + kFormGridFlat)
@@ -1006,16 +975,8 @@ static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, f
     X(11, kFormGridSlow) X(12, kFormGridSlow) X(13, kFormGridSlow)                                            \
     X(11, kFormGridWide) X(13, kFormGridWide) X(11, kFormGridWideSlow) X(13, kFormGridWideSlow)               \
     MM_FLAT_INSTANCES(X) X(3, kFormLean)
-#ifdef MM_AB_VARIANTS
-#define MM_WP_INSTANCES(X)                                                                                    \
-    MM_DEFER_INSTANCES(X) X(6, kFormLean) X(7, kFormLean) X(10, kFormLean)                                    \
-    X(0, kFormLeafInterior) X(1, kFormLeafInterior) X(3, kFormLeafInterior) X(6, kFormLeafInterior)           \
-    X(7, kFormLeafInterior) X(10, kFormLeafInterior)                                                          \
-    X(1, kFormIfIf) X(3, kFormIfIf)
-#else
 #define MM_WP_INSTANCES(X)                                                                                    \
     MM_DEFER_INSTANCES(X) X(0, kFormLeafInterior) X(1, kFormLeafInterior) X(3, kFormLeafInterior)
-#endif
 
 bool wavepersist_built(int lds_mode, int form) {
 #define MM_WP(L, F) if (lds_mode == L && form == F) return true;
@@ -1066,41 +1027,16 @@ hipError_t wavepersist_attributes(int lds_mode, int form, int ring, hipFuncAttri
     return hipErrorInvalidValue;
 }
 
-template <bool kRef, bool kLds>
-static void launch_mega_t(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats,
-                          uint32_t* err, bool count_stats, uint32_t block, hipStream_t s) {
-    const uint32_t n = job.w * job.h * job.e.spp;
-    const dim3 grid((n + block - 1) / block);
-    const size_t lds = kLds ? 2 * (size_t)sc.n_nodes * sizeof(float4) : 0;
-    if (count_stats)
-        hipLaunchKernelGGL((k_trace_mega<true, kRef, kLds>), grid, dim3(block), lds, s, sc, job, samples, stats, err);
-    else
-        hipLaunchKernelGGL((k_trace_mega<false, kRef, kLds>), grid, dim3(block), lds, s, sc, job, samples, stats, err);
-}
-
 hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats_dev,
                              uint32_t* err, bool count_stats, const MegaOpts& o, hipStream_t s) {
-    if (o.reference) {
-        launch_mega_t<true, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
-        return hipGetLastError();
-    }
-#ifdef MM_AB_VARIANTS
-    if (o.lds_nodes)
-        launch_mega_t<false, true>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
+    if (!o.reference) return hipErrorInvalidValue;  // one thread per path: MM_PIPE_REFERENCE only
+    const uint32_t n = job.w * job.h * job.e.spp;
+    const dim3 grid((n + o.block - 1) / o.block);
+    if (count_stats)
+        hipLaunchKernelGGL(k_trace_mega<true>, grid, dim3(o.block), 0, s, sc, job, samples, stats_dev, err);
     else
-        launch_mega_t<false, false>(sc, job, samples, stats_dev, err, count_stats, o.block, s);
+        hipLaunchKernelGGL(k_trace_mega<false>, grid, dim3(o.block), 0, s, sc, job, samples, stats_dev, err);
     return hipGetLastError();
-#else
-    return hipErrorInvalidValue;  // one thread per path: A/B build only
-#endif
-}
-
-bool ab_variants_built() {
-#ifdef MM_AB_VARIANTS
-    return true;
-#else
-    return false;
-#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -43,6 +43,7 @@ MM_INFO_GRID_OK, MM_INFO_GRID_CELLS_X, MM_INFO_GRID_CELLS_Y, MM_INFO_GRID_CELLS_
 MM_INFO_GRID_GLOBAL, MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_LEAN, MM_INFO_DEPTH = 5, 6, 7, 8, 9
 MM_INFO_DICT_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE, MM_INFO_GRID_FACES = 10, 11, 12, 13
 MM_INFO_LAST_DEFER, MM_INFO_LAST_VGPRS, MM_INFO_LAST_SCRATCH, MM_INFO_LAST_STATIC_LDS = 14, 15, 16, 17
+MM_INFO_GRID_LDS_CAP = 18
 MM_PLAYER_COLLIDED, MM_PLAYER_ROTATED, MM_PLAYER_NAN_QUAT = 1, 2, 4
 MM_BVH_SWEEP, MM_BVH_EXHAUSTIVE = 0, 1
 MM_OWN_STREAM = C.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value  # (void*)-1
@@ -129,6 +130,7 @@ EXPORTS = {
     "mm_comm_init_all": (C.c_int, [C.c_int, P, P]),
     "mm_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mm_comm_rccl_version": (C.c_int, []),
+    "mm_comm_rccl_header_version": (C.c_int, []),
     "mm_comm_destroy": (None, [P]),
     "mm_row_shard": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
@@ -183,11 +185,6 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
-
-
-def ab_variants() -> bool:
-    """True when the library was built with -DMM_AB_VARIANTS (A/B-only kernels)."""
-    return lib().mm_version().decode().endswith("+ab")
 
 
 def check(rc: int, ctx=None) -> None:

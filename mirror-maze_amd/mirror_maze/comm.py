@@ -63,15 +63,30 @@ class _OnStream:
         lib().mm_set_stream(self.r._ctx, self.old)
 
 
-def _tile_shape(t):
+def _tile_shape(t, height: int = 0, n_ranks: int = 0):
     """(n_frames, rows_max, width, bytes_per_px) of a (F, rows_max, W, C) or
-    (rows_max, W, C) contiguous CUDA tensor."""
+    (rows_max, W, C) contiguous CUDA tensor.  With height and n_ranks, the
+    tile must hold exactly rows_max = ceil(height / n_ranks) rows: the C side
+    sizes every rank's slab from the height alone, so a shorter tile (a
+    ragged rank's tile[:rows]) would be read past its end."""
     if not (t.is_cuda and t.is_contiguous()):
         raise ValueError("tiles must be contiguous CUDA tensors")
     shape = tuple(t.shape) if t.dim() == 4 else (1,) + tuple(t.shape)
     if len(shape) != 4:
         raise ValueError("tile must be (frames, rows, width, channels) or (rows, width, channels)")
+    if n_ranks:
+        rm = row_shard(height, n_ranks, 0)[3]
+        if shape[1] != rm:
+            raise ValueError(f"tile has {shape[1]} rows; every rank's tile must hold rows_max = {rm} rows "
+                             f"(height {height} over {n_ranks} ranks; pad the short ranks' tiles)")
     return shape[0], shape[1], shape[2], shape[3] * t.element_size()
+
+
+def _check_out(out, tile, nf: int, height: int):
+    """rank 0's frame buffer: contiguous CUDA, the tile's dtype, (nf, height, W, C) elements."""
+    if not (out.is_cuda and out.is_contiguous() and out.dtype == tile.dtype
+            and out.numel() == nf * height * tile.shape[-2] * tile.shape[-1]):
+        raise ValueError("out must be a contiguous (frames, height, width, channels) tensor of the tile dtype")
 
 
 class Comm:
@@ -113,6 +128,10 @@ class Comm:
     def rccl_version() -> int:
         return lib().mm_comm_rccl_version()
 
+    @staticmethod
+    def rccl_header_version() -> int:
+        return lib().mm_comm_rccl_header_version()
+
     def gather_rows(self, tile, height: int, out=None, stream=None, self_via_rccl: bool = False):
         """Frame-end gather (mm_gather_rows) of this rank's tile -- (F, rows_max,
         W, C) or (rows_max, W, C), rows rank, rank + N, ... of each frame -- into
@@ -121,13 +140,12 @@ class Comm:
         (default: the renderer's stream, or torch's current one)."""
         import torch
 
-        nf, rows_max, w, bpp = _tile_shape(tile)
+        nf, rows_max, w, bpp = _tile_shape(tile, height, self.n_ranks)
         if self.rank == 0:
             if out is None:
                 out = torch.empty((nf, height) + tuple(tile.shape[-2:]), dtype=tile.dtype, device=tile.device)
-            elif not (out.is_cuda and out.is_contiguous() and out.dtype == tile.dtype
-                      and out.numel() == nf * height * w * tile.shape[-1]):
-                raise ValueError("out must be a contiguous (frames, height, width, channels) tensor of the tile dtype")
+            else:
+                _check_out(out, tile, nf, height)
         flags = _lib.MM_GATHER_SELF_VIA_RCCL if self_via_rccl else 0
         r = self.renderer
         with _OnStream(r, _stream_of(r, stream)):
@@ -151,11 +169,20 @@ def gather_rows_all(comms, tiles, height: int, out=None, self_via_rccl: bool = F
     import torch
 
     n = len(comms)
+    if len(tiles) != n:
+        raise ValueError("one tile per communicator")
     root = [c.rank for c in comms].index(0)
-    nf, rows_max, w, bpp = _tile_shape(tiles[root])
+    t = tiles[root]
+    nf, rows_max, w, bpp = _tile_shape(t, height, n)
+    for i, ti in enumerate(tiles):  # every rank's tile: the root's shape and dtype (the C side assumes it)
+        if tuple(ti.shape) != tuple(t.shape) or ti.dtype != t.dtype or ti.device.index != comms[i].renderer.device:
+            raise ValueError(f"tile {i}: every rank's tile must have the root tile's shape and dtype, "
+                             f"on its communicator's GPU")
+        _tile_shape(ti, height, n)
     if out is None:
-        t = tiles[root]
         out = torch.empty((nf, height) + tuple(t.shape[-2:]), dtype=t.dtype, device=t.device)
+    else:
+        _check_out(out, t, nf, height)
     rens = [c.renderer for c in comms]
     ctxs = (C.c_void_p * n)(*[r._ctx.value for r in rens])
     hs = (C.c_void_p * n)(*[c._h.value for c in comms])
@@ -180,8 +207,13 @@ def assemble_rows(renderer, tiles, height: int, out=None, stream=None):
     if tiles.dim() != 5 or not (tiles.is_cuda and tiles.is_contiguous()):
         raise ValueError("tiles must be a contiguous (ranks, frames, rows_max, width, channels) CUDA tensor")
     n, nf, rows_max, w, ch = tiles.shape
+    if rows_max != row_shard(height, n, 0)[3]:
+        raise ValueError(f"tiles hold {rows_max} rows; {n} ranks of a {height}-row frame need rows_max = "
+                         f"{row_shard(height, n, 0)[3]}")
     if out is None:
         out = torch.empty((nf, height, w, ch), dtype=tiles.dtype, device=tiles.device)
+    else:
+        _check_out(out, tiles[0], nf, height)
     with _OnStream(renderer, _stream_of(renderer, stream)):
         check(lib().mm_assemble_rows(renderer._ctx, tiles.data_ptr(), n, nf, w, height, ch * tiles.element_size(),
                                      out.data_ptr()), renderer._ctx)
@@ -190,8 +222,7 @@ def assemble_rows(renderer, tiles, height: int, out=None, stream=None):
 
 class NativeGatherer:
     """bench.py's frame path over the library's gather (one per multi-frame
-    launch, or per frame with n = 1), the same interface as
-    mirror_maze.dist.BatchGatherer: ``tiles(n)`` hands out the (n, rows_max,
+    launch, or per frame with n = 1): ``tiles(n)`` hands out the (n, rows_max,
     W, C) slice of a rotating slot buffer the launch's frames go into (after
     the gather that last read the slot is done), ``put(n)`` issues the gather
     on ``gather_stream`` once the current stream's work on the tiles is done,
@@ -251,3 +282,63 @@ class NativeGatherer:
             return None
         slot, n = self.last
         return self.frames[slot][n - 1]
+
+
+class HostComm:
+    """Diagnostics transport with Comm's interface, for N ranks that share ONE
+    GPU (bench.py --shared-gpu).  RCCL refuses two ranks on one device, so
+    here the tiles cross between the ranks' processes as host copies over
+    torch.distributed point-to-point (gloo), and rank 0 de-interleaves them
+    with the library's mm_assemble_rows -- the kernel mm_gather_rows ends in.
+    Everything around it (NativeGatherer's slots and events, the rank >= 1
+    branches of bench.py, the exposed-gather clock, the reductions) is the
+    product's N-GPU path unchanged, so one GPU box can execute it end to end.
+    Not a product transport: its host round trip makes any timing of it
+    meaningless."""
+
+    def __init__(self, renderer, n_ranks: int, rank: int, group=None):
+        if not (0 <= rank < n_ranks):
+            raise ValueError("rank out of range")
+        self.renderer, self.n_ranks, self.rank, self.group = renderer, n_ranks, rank, group
+        self.device = getattr(renderer, "device", None)
+
+    def exchange(self, host_tile):
+        """Every rank's host tile to rank 0 (which gets them in rank order);
+        None on the other ranks.  Blocking, torch.distributed send / recv."""
+        import torch
+        import torch.distributed as dist
+
+        if self.rank != 0:
+            dist.send(host_tile, 0, group=self.group)
+            return None
+        parts = [host_tile] + [torch.empty_like(host_tile) for _ in range(1, self.n_ranks)]
+        for r in range(1, self.n_ranks):
+            dist.recv(parts[r], r, group=self.group)
+        return parts
+
+    def gather_rows(self, tile, height: int, out=None, stream=None, self_via_rccl: bool = False):
+        """Comm.gather_rows's contract (same checks, same result on rank 0),
+        over the host transport; enqueued on / synchronised with `stream`."""
+        import torch
+
+        nf, rows_max, w, bpp = _tile_shape(tile, height, self.n_ranks)
+        if self.rank == 0:
+            if out is None:
+                out = torch.empty((nf, height) + tuple(tile.shape[-2:]), dtype=tile.dtype, device=tile.device)
+            else:
+                _check_out(out, tile, nf, height)
+        t5 = tile if tile.dim() == 4 else tile.unsqueeze(0)
+        s = torch.cuda.current_stream(tile.device) if stream is None else stream
+        with torch.cuda.stream(s):
+            host = t5.cpu()  # (waits for the stream's work on the tile)
+        parts = self.exchange(host)
+        if self.rank != 0:
+            return None
+        with torch.cuda.stream(s):
+            staged = torch.stack(parts).to(tile.device)  # (N, F, rows_max, W, C)
+            assemble_rows(self.renderer, staged, height, out=out.view((nf, height) + tuple(tile.shape[-2:])),
+                          stream=s)
+        return out
+
+    def close(self) -> None:
+        pass

@@ -26,10 +26,6 @@ VARIANTS = {
     "grid-global": (1, {7: 11, 1: 0}),
     "bvh-lean": (1, {7: 7}),
     "bvh-li": (1, {7: 5}),
-    "bvh-ifif": (1, {7: 0}),
-    "bvh-lean-dict": (1, {7: 7, 20: 2}),
-    "bvh-li-split": (1, {7: 5, 9: 80}),
-    "mega-lds": (1, {3: 0, 1: 1}),
     "nofuse": (1, {12: 0}),
     "nodefer": (1, {21: 0}),
     "defer8": (1, {21: 8}),

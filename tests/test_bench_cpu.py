@@ -51,8 +51,9 @@ def test_pmc_record_of_other_sources_is_marked_stale(monkeypatch):
 
 
 def test_pmc_record_per_emulated_rank_share(monkeypatch):
-    """--emulate-ranks N reads pmc_<config>_r<N>.json (rank 0's own launch
-    shape), not the whole frame's record; without one there is no record."""
+    """--emulate-ranks N and world = N both read pmc_<config>_r<N>.json (rank
+    0's own launch shape), not the whole frame's record; without one there is
+    no record."""
     import json
 
     import bench
@@ -61,10 +62,56 @@ def test_pmc_record_per_emulated_rank_share(monkeypatch):
     monkeypatch.setattr(bench, "src_hash", lambda: rec["src_hash"])
     m, _ = bench.pmc_profile(_args(emulate_ranks=8), 20, 0.0065, 1)
     assert m["source"] == "profiles/pmc_c3_r8.json"
-    m, traffic = bench.pmc_profile(_args(emulate_ranks=4), 20, 0.013, 1)
+    m, _ = bench.pmc_profile(_args(), 20, 0.0065, 8)  # world = 8: rank 0's launch shape, the same record
+    assert m["source"] == "profiles/pmc_c3_r8.json"
+    m, traffic = bench.pmc_profile(_args(), 20, 0.013, 3)  # no record of rank 0 of 3
     assert m["source"] is None and traffic is None
-    m, _ = bench.pmc_profile(_args(), 20, 0.05, 8)  # N > 1 ranks: no single-GPU record applies
+    m, _ = bench.pmc_profile(_args(), 20, 0.0065, 8, shared=True)  # diagnostics: never a roofline
     assert m["source"] is None
+
+
+def _frac_keys(d, path=""):
+    """Every (path, value) of a key named "frac" in a nested dict."""
+    out = []
+    for k, v in d.items():
+        if isinstance(v, dict):
+            out += _frac_keys(v, f"{path}.{k}")
+        elif k == "frac" and v is not None:
+            out.append((f"{path}.{k}", v))
+    return out
+
+
+def test_roofline_at_eight_ranks_is_the_executed_basis(monkeypatch):
+    """the N = 8 line's roofline reads rank 0's PMC record
+    (pmc_c3_r8.json) and quotes executed lane-ops like N = 1 -- at the
+    record's own launch time its frac equals the record's profile_frac within
+    1 % -- and no printed fraction passes 1 (the models carry model_ratio)."""
+    import json
+
+    import bench
+
+    rec = json.loads((bench.REPO / "profiles" / "pmc_c3_r8.json").read_text())
+    monkeypatch.setattr(bench, "src_hash", lambda: rec["src_hash"])
+    k_avg = rec["kernel_avg_ms"] / 1e3
+    fpl = rec["frames_per_launch"]
+    m, traffic = bench.pmc_profile(_args(), fpl, k_avg, 8)
+    # a reference-walk model far above the peak and an HBM model above it: printed as ratios only
+    r = bench.roofline(120e12 * k_avg, 9e12 * k_avg, k_avg, 1, fpl, m, traffic, 1, {})
+    assert r["basis"].startswith("executed") and "pmc_c3_r8.json" in r["basis"]
+    assert abs(r["frac"] / m["profile_frac"] - 1) < 0.01, (r["frac"], m["profile_frac"])
+    assert r["unit"] == "T lane-ops/s"
+    assert r["reference_equivalent"]["model_ratio"] > 1 and r["model_hbm"]["model_ratio"] > 1
+    fracs = _frac_keys(r)
+    assert fracs and all(0 <= v <= 1 for _, v in fracs), fracs
+
+
+def test_roofline_without_a_record_is_null_not_a_model():
+    import bench
+
+    m = {"source": None, "note": "no PMC record for this launch shape"}
+    r = bench.roofline(40e12 * 0.05, 1e9, 0.05, 1, 20, m, None, 1, {})
+    assert r["achieved"] is None and r["frac"] is None and r["basis"].startswith("none")
+    assert r["reference_equivalent"]["model_ratio"] == round(40 / bench.VALU_PEAK_TOPS, 4)
 
 
 def _largs(gpus=1, launcher="auto"):
@@ -136,13 +183,14 @@ def test_child_relay_passes_rank0_line_and_exit_status(tmp_path):
 
 def test_stale_record_is_never_the_headline():
     """with a PMC record of other sources the roofline headline
-    is the reference-walk model; the stale lane-ops rate sits only in the
-    labelled stale_profile sub-object and the line carries stale: true."""
+    is null (never a model); the stale lane-ops rate sits
+    only in the labelled stale_profile sub-object and the line carries
+    stale: true."""
     import bench
 
     measured = {"source": "profiles/pmc_c3.json", "stale": True, "stale_valu_lane_ops_tops": 30.0}
     r = bench.roofline(40e12 * 0.05, 1e9, 0.05, 1, 20, measured, None, 1, {})
-    assert r["stale"] is True and r["achieved"] == 40.0 and r["basis"].startswith("reference_equivalent")
+    assert r["stale"] is True and r["achieved"] is None and r["frac"] is None and r["basis"].startswith("none")
     assert r["stale_profile"]["valu_lane_ops_tops"] == 30.0
-    fresh = bench.roofline(40e12 * 0.05, 1e9, 0.05, 1, 20, {"valu_lane_ops_tops": 29.0}, 5, 1, {})
+    fresh = bench.roofline(40e12 * 0.05, 1e9, 0.05, 1, 20, {"valu_lane_ops_tops": 29.0, "source": "x"}, 5, 1, {})
     assert fresh["stale"] is False and fresh["achieved"] == 29.0 and fresh["stale_profile"] is None

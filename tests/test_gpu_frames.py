@@ -101,18 +101,14 @@ def test_c4_rank0_of_eight_way_split(gpu):
 C5_WINDOWS = [(0, 0), (1904, 1064), (3808, 2144), (700, 1500), (2900, 300), (1200, 40)]
 
 
-@pytest.mark.parametrize("opts", [{}, {21: 32, 22: 0}, {7: 7}], ids=["auto", "tail-deferral", "bvh-walk"])
+@pytest.mark.parametrize("opts", [{}, {21: 32, 22: 0}, {7: 5}], ids=["auto", "tail-deferral", "bvh-walk"])
 def test_c5_windows_64spp(gpu, opts):
     """C5: 64x64 maze, 3840x2160 frame coordinates, 64 spp, 16/16 bounces --
     the reference's 64-sample reduction (shaders.metal:342-364) as the fused
-    resolve, one pixel per wave -- on six 32x16 windows.  "bvh-walk": the
-    lean BVH form over dictionary nodes (A/B build) or loop form 5 over nodes
-    read through L1/L2 (default build: form 7 needs the N=64 tree in LDS)."""
-    from mirror_maze import Renderer, ab_variants, default_uniform, make_ext
+    resolve, one pixel per wave -- on six 32x16 windows.  "bvh-walk": loop
+    form 5 over nodes read through L1/L2 (form 7 needs the N=64 tree in LDS)."""
+    from mirror_maze import Renderer, default_uniform, make_ext
     from oracle.oracle import Oracle
-
-    if opts.get(7) == 7 and not ab_variants():
-        opts = {7: 5}
 
     s = _scene(64)
     o = Oracle.from_scene(s)

@@ -104,14 +104,15 @@ WINDOWS = [(0, 0), (960, 540), (1888, 1064), (300, 700), (1500, 100)]
 
 
 # (pipeline, {option: value}, exact_counts); options (include/mm_api.h): 1 LDS,
-# 3 persist, 7 traversal (-1 auto, 0, 5, 7 BVH loop forms, 11 grid search),
-# 8 LDS rect records, 9 split-cache KB, 12 fused resolve, 20 dictionary nodes.
+# 7 traversal (-1 auto, 5, 7 BVH loop forms, 11 grid search), 8 LDS rect
+# records, 12 fused resolve, 21 / 22 tail deferral.  (The A/B-only variants --
+# one thread per path, loop form 0, split node cache, dictionary nodes, form 7
+# with global records -- were removed in round 6; the
+# options that chose them fail: test_removed_variants_refused.)
 # exact_counts: node visits and rect tests equal the oracle's (BVH walks); the
 # grid search counts its own work (cells, rect tests), only rays and paths match.
 PIPES = {
     "reference": (3, {}, True),
-    "mega-global": (1, {1: 0, 3: 0}, True),
-    "mega-lds": (1, {1: 1, 3: 0}, True),
     "auto": (0, {}, False),                                  # grid search (C3 default)
     "grid": (1, {7: 11}, False),
     "grid-nofuse": (1, {7: 11, 12: 0}, False),
@@ -122,39 +123,17 @@ PIPES = {
     "grid-defer64": (1, {21: 64, 22: 0}, False),             # every path at bounce 1: tail rings run full
     "bvh-lean-defer32": (1, {7: 7, 21: 32, 22: 0}, True),
     "bvh-lean-ldsrects": (1, {7: 7}, True),
-    "bvh-lean-globalrecs": (1, {7: 7, 8: 0}, True),
-    "bvh-lean-split2kb": (1, {7: 7, 9: 2}, True),
-    "bvh-lean-dict": (1, {7: 7, 20: 2}, True),
     "bvh-li-ldsrects": (1, {7: 5}, True),
     "bvh-li-globalrecs": (1, {7: 5, 8: 0}, True),
     "bvh-li-global": (1, {7: 5, 1: 0}, True),
-    "bvh-li-split2kb": (1, {7: 5, 9: 2}, True),
-    "bvh-li-dict": (1, {7: 5, 20: 2}, True),
-    "bvh-ifif-ldsrects": (1, {7: 0}, True),
-    "bvh-ifif-lds": (1, {7: 0, 8: 0}, True),
     "wavefront": (2, {}, False),                             # mirror-tail deferral always on
     "wavefront-global": (2, {1: 0}, False),
 }
 
 
-# Variants built only with `make EXTRA=-DMM_AB_VARIANTS`: the
-# default library holds the kernels MM_PIPE_AUTO can select.
-AB_ONLY = {"mega-global", "mega-lds", "bvh-lean-globalrecs", "bvh-lean-split2kb", "bvh-lean-dict",
-           "bvh-li-split2kb", "bvh-li-dict", "bvh-ifif-ldsrects", "bvh-ifif-lds"}
-
-
-def _need_ab(what):
-    from mirror_maze import ab_variants
-
-    if not ab_variants():
-        pytest.skip(f"{what}: A/B-only variant (library built without -DMM_AB_VARIANTS)")
-
-
 def _renderer(pipe, scene):
     from mirror_maze import Renderer
 
-    if pipe in AB_ONLY:
-        _need_ab(pipe)
     r = Renderer(0)
     p, opts, _ = PIPES[pipe]
     r.set_pipeline(p)
@@ -192,7 +171,7 @@ def test_tile_windows_bit_exact(gpu, cfg, pipe):
 
 
 @pytest.mark.parametrize("pipe", ["auto", "grid-nofuse", "grid-nodefer", "grid-defer", "grid-defer64",
-                                  "bvh-lean-ldsrects", "bvh-li-dict", "mega-lds", "wavefront"])
+                                  "bvh-lean-ldsrects", "bvh-li-global", "reference", "wavefront"])
 def test_small_full_frames_bit_exact(gpu, pipe):
     """Whole 256x144 frames (8 spp, 8/8 bounces, 3 frames, N=32 maze): ~7 M
     closest-hit queries per pipeline against the oracle, so rare boundary
@@ -236,19 +215,17 @@ def test_tiling_and_device_count_invariance_full_frame(ren, gpu):
     assert np.isfinite(img).all() and (img[..., :3] >= 0).all() and np.all(img[..., 3] == 1.0)
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 5, 9: 2}, {7: 7}, {19: 8}, {21: 0}, {21: 32, 22: 0}])
+@pytest.mark.parametrize("opts", [{}, {7: 5}, {7: 5, 1: 0}, {7: 7}, {19: 8}, {21: 0}, {21: 32, 22: 0}])
 def test_multi_frame_launch_bit_identical(gpu, opts):
     """mm_trace_tile_frames: F frames in one launch (one work queue) equal the
     F single-frame launches bit for bit, with summed work counts -- C3 whole
-    frames and a row-split tile; the grid search (default), the split node
-    cache with loop form 5, the lean BVH form; a grid 8 CUs short
+    frames and a row-split tile; the grid search (default), loop form 5 with
+    the nodes in LDS and through L1/L2, the lean BVH form; a grid 8 CUs short
     (MM_OPT_RESERVE_CUS)."""
     import torch
 
     from mirror_maze import Renderer, default_uniform, make_ext
 
-    if opts.get(9, 0) > 1:
-        _need_ab("split node cache")
     s = _scene(32)
     r = Renderer(0)
     for k, v in opts.items():
@@ -361,23 +338,17 @@ def test_argument_errors(ren, gpu):
     assert ei.value.code == -5  # MM_ERR_STACK
 
 
-@pytest.mark.parametrize("opts", [{}, {7: 5}, {7: 7}, {7: 5, 20: 0}, {7: 5, 9: 8}, {7: 5, 9: 0},
-                                  {7: 5, 1: 0}, {3: 0}, {7: 11, 1: 0}],
-                         ids=["auto", "li-dict", "lean-dict", "li-split", "li-split-8kb", "li-global-nodes",
-                              "li-nothing-in-lds", "mega", "grid-not-in-lds"])
+@pytest.mark.parametrize("opts", [{}, {7: 5}, {7: 5, 1: 0}, {7: 11, 1: 0}],
+                         ids=["auto", "li-global-nodes", "li-nothing-in-lds", "grid-not-in-lds"])
 def test_large_scene_bit_exact(gpu, opts):
     """C5's N=64 maze: the grid image (cells, lists, records, leaf boxes) and
     the BVH (5.5 k nodes, 177 KB) exceed the LDS budget.  Auto runs the grid
-    search with its index in LDS and records / leaf boxes through L1/L2; the
-    BVH forms use dictionary nodes, the top-of-tree cache or global nodes.
+    search with its index in LDS and records / leaf boxes through L1/L2; loop
+    form 5 reads the nodes through L1/L2.
     Bit-exact vs the oracle at C5 limits (16/16 bounces) on 4 windows."""
     from mirror_maze import MM_INFO_GRID_BYTES, MM_INFO_GRID_INDEX_BYTES, MM_INFO_GRID_OK, default_uniform, make_ext
     from oracle.oracle import Oracle
 
-    dict_auto = opts.get(7) == 5 and opts.get(20, 1) and opts.get(9, 1) and opts.get(1, 1)  # "li-dict"
-    if opts.get(9, 0) > 1 or opts.get(3) == 0 or opts.get(7) == 7 or dict_auto:
-        _need_ab("N=64 BVH placement (dictionary nodes, split cache, lean form with global records, "
-                 "one thread per path)")
     s = _scene(64)
     assert s.n_nodes * 32 > 160 * 1024
     o = Oracle.from_scene(s)
@@ -396,7 +367,7 @@ def test_large_scene_bit_exact(gpu, opts):
         ref, rst = o.trace_tile(u, e, x0, y0, 32, 16)
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
         assert st.rays == rst.rays
-        if opts.get(7) in (5, 7) or opts.get(3) == 0:
+        if opts.get(7) in (5, 7):
             assert (st.node_visits, st.rect_tests) == (rst.node_visits, rst.rect_tests)
     r.close()
 
@@ -458,9 +429,11 @@ def test_bench_prints_one_json_line(gpu):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["unit"] == "Mrays/s" and d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2
-    assert d["roofline"]["bound"] == "valu" and 0 < d["roofline"]["frac"] < 1
-    assert d["roofline"]["model_hbm"]["bytes_per_ray"] == 136 and "measured" in d["roofline"]
-    assert 0 < d["roofline"]["reference_equivalent"]["frac"] < 1 and d["roofline"]["basis"]
+    # (a C2 line: executed lane-ops from profiles/pmc_c2.json when it holds these sources, else null)
+    rf = d["roofline"]
+    assert rf["bound"] == "valu" and (rf["frac"] is None or 0 < rf["frac"] < 1) and rf["basis"]
+    assert rf["model_hbm"]["bytes_per_ray"] == 136 and "measured" in rf
+    assert rf["reference_equivalent"]["model_ratio"] > 0
     kr = d["roofline"]["kernel_resources"]
     assert 0 < kr["vgprs_per_lane"] <= 64 and kr["scratch_bytes_per_lane"] >= 0
     assert d["distributed"] is None  # one process, no torchrun
@@ -506,3 +479,23 @@ def test_trace_tile_rejects_limits_beyond_the_packed_state(gpu):
                 r.trace_tile(u, make_ext(1, bl, ml), 0, 0, 4, 4)
         img, _ = r.trace_tile(u, make_ext(1, 32767, 8), 0, 0, 4, 4)  # the bound itself is accepted
         assert img.shape == (4, 4, 4)
+
+
+def test_removed_variants_refused(gpu):
+    """the A/B-only kernel variants were deleted; the
+    option values that chose them fail with MM_ERR_UNSUPPORTED (-6) by name,
+    the values that select nothing are still accepted, and the version string
+    carries no A/B marker."""
+    from mirror_maze import MM_INFO_DICT_OK, MMError, Renderer, lib
+
+    assert "+ab" not in lib().mm_version().decode()
+    r = Renderer(0)
+    for key, val in [(3, 0), (7, 0), (9, 2), (20, 2)]:
+        with pytest.raises(MMError) as ei:
+            r.set_option(key, val)
+        assert ei.value.code == -6 and "removed" in str(ei.value), (key, val)
+    for key, val in [(3, 2), (7, 5), (9, 0), (9, 1), (20, 0), (20, 1)]:
+        r.set_option(key, val)
+    r.upload_scene(_scene(10))
+    assert r.scene_info(MM_INFO_DICT_OK) == 0.0
+    r.close()

@@ -1,7 +1,7 @@
 """Parity on scenes that are not mazes: random soups of axis-aligned rects
 (with the reference's own SAH BVH over them, Scene.bvh).  They exercise what
-the maze does not: thousands of distinct bound values (no dictionary nodes:
-the BVH forms fall back to the top-of-tree cache), grid lists of
+the maze does not: thousands of distinct bound values (BVH nodes too large
+for LDS: the BVH forms read them through L1/L2), grid lists of
 arbitrary rects, and -- in the lattice scene -- many coplanar overlapping
 rects, whose equal hit distances are ties the certified grid search must
 hand to the reference walk.  Bit-exact vs the oracle."""
@@ -43,36 +43,26 @@ def random_scene(n, seed, lattice):
 
 
 # per scene: options -> (query method run, LDS modes it may use) or None when the
-# method is unavailable (form 7 needs a compact record for every rect: the fine
-# scene's rects have normals that are not exactly +-1, SLOW records).  The
-# BVH's 192 KB of nodes exceed the LDS budget: the A/B build places them as
-# dictionary nodes (mode 10) or the top-of-tree cache (6); the default build
-# reads them through L1/L2 (mode 0, form 5; form 7 needs nodes + records in LDS).
+# method is unavailable (form 7 needs a compact record for every rect -- the fine
+# scene's rects have normals that are not exactly +-1, SLOW records -- and the
+# nodes + records in LDS: the BVH's 192 KB of nodes exceed the LDS budget, so
+# loop form 5 reads them through L1/L2, mode 0).
 CASES = {
     "auto-grid": ({}, {False: (11, (11, 12)), True: (11, (11, 12))}),
-    "bvh-lean": ({7: 7}, {False: None, True: (7, (10,))}),
-    "bvh-li": ({7: 5}, {False: (5, (6,)), True: (5, (10,))}),
-    "bvh-li-nodict": ({7: 5, 20: 0, 9: 0}, {False: (5, (0,)), True: (5, (0,))}),
+    "bvh-lean": ({7: 7}, {False: None, True: None}),
+    "bvh-li": ({7: 5}, {False: (5, (0,)), True: (5, (0,))}),
     "grid-global": ({7: 11, 1: 0}, {False: (11, (13,)), True: (11, (13,))}),
-}
-CASES_DEFAULT_BUILD = {
-    "bvh-lean": {False: None, True: None},
-    "bvh-li": {False: (5, (0,)), True: (5, (0,))},
 }
 
 
 @pytest.mark.parametrize("lattice", [False, True], ids=["fine", "lattice"])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_random_scene_windows_bit_exact(gpu, lattice, case):
-    from mirror_maze import (MM_INFO_DICT_OK, MM_INFO_GRID_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE,
-                             MM_INFO_LEAN, MMError, Renderer, default_uniform, make_ext)
+    from mirror_maze import (MM_INFO_GRID_OK, MM_INFO_LAST_FORM, MM_INFO_LAST_LDS_MODE, MM_INFO_LEAN, MMError,
+                             Renderer, default_uniform, make_ext)
     from oracle.oracle import Oracle
 
-    from mirror_maze import ab_variants
-
     opts, expect = CASES[case]
-    if not ab_variants():
-        expect = CASES_DEFAULT_BUILD.get(case, expect)
     expect = expect[lattice]
     s = random_scene(3000, 11 if lattice else 7, lattice)
     o = Oracle.from_scene(s)
@@ -81,8 +71,6 @@ def test_random_scene_windows_bit_exact(gpu, lattice, case):
         r.set_option(k, v)
     r.upload_scene(s)
     assert r.scene_info(MM_INFO_GRID_OK) == 1.0
-    # (MM_OPT_DICT_NODES 0 at upload: the dictionary is not built)
-    assert r.scene_info(MM_INFO_DICT_OK) == (1.0 if lattice and opts.get(20, 1) != 0 else 0.0)
     assert r.scene_info(MM_INFO_LEAN) == (1.0 if lattice else 0.0)
     u = default_uniform(1920, 1080, 0)
     e = make_ext(8, 8, 8, frame=3)
@@ -127,3 +115,50 @@ def test_scene_reaching_2_60_takes_the_bvh_bit_exact(gpu):
         assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (x0, y0)
         assert (st.rays, st.paths) == (rst.rays, rst.paths)
     r.close()
+
+
+def test_grid_images_fit_the_static_lds_array(gpu):
+    """LDS placements 11 / 14 stage the grid image into a static
+    array (MM_INFO_GRID_LDS_CAP bytes, a little under 80 KB); the grid builder
+    now takes that capacity as its budget, so no image between it and 80 KB
+    can be built and then refused at launch.  Mazes and random soups over a
+    sweep of cell sizes give many image sizes near the budget: every one is
+    within the capacity wherever a whole-image placement runs, and every
+    upload traces (whole-frame sample windows, bit-exact vs the oracle for a
+    few)."""
+    from mirror_maze import (MM_INFO_GRID_BYTES, MM_INFO_GRID_FACES, MM_INFO_GRID_LDS_CAP, MM_INFO_GRID_OK,
+                             MM_INFO_LAST_LDS_MODE, Renderer, Scene, default_uniform, make_ext)
+    from oracle.oracle import Oracle
+
+    u = default_uniform(1920, 1080, 0)
+    e = make_ext(4, 6, 6, frame=1)
+    checked = 0
+    sizes = []
+    scenes = [("maze24", Scene.build(24, 0)), ("maze40", Scene.build(40, 0)),
+              ("soup", random_scene(1500, 3, False))]
+    for name, s in scenes:
+        o = None
+        for cell in range(40, 241, 25):
+            r = Renderer(0)
+            r.set_option(25, cell)
+            r.upload_scene(s)
+            if r.scene_info(MM_INFO_GRID_OK) != 1.0:
+                r.close()
+                continue
+            cap = r.scene_info(MM_INFO_GRID_LDS_CAP)
+            assert 79 * 1024 < cap < 80 * 1024
+            nbytes = r.scene_info(MM_INFO_GRID_BYTES)
+            if r.scene_info(MM_INFO_GRID_FACES):
+                assert nbytes <= cap, (name, cell, nbytes, cap)
+            got, _ = r.trace_tile(u, e, 944, 532, 32, 16)
+            mode = r.scene_info(MM_INFO_LAST_LDS_MODE)
+            if mode in (11, 14):
+                assert nbytes <= cap or mode == 14, (name, cell, nbytes, mode)
+            sizes.append((name, cell, int(nbytes), int(mode)))
+            if checked < 4:
+                o = o or Oracle.from_scene(s)
+                ref, _ = o.trace_tile(u, e, 944, 532, 32, 16)
+                assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref)), (name, cell)
+                checked += 1
+            r.close()
+    assert len(sizes) >= 12, sizes

@@ -104,3 +104,50 @@ def test_bench_distributed_path_delivers_the_frame(gpu, tmp_path, config, launch
     assert got.dtype == np.uint8 and got.shape == (H, W, 4)
     assert np.array_equal(got, want8)
     r.close()
+
+
+@pytest.mark.parametrize("n_ranks", [2, 8])
+def test_bench_n_ranks_on_one_gpu_run_the_n_gpu_path(gpu, tmp_path, n_ranks):
+    """the product's N-rank path executed end to end on
+    one GPU.  `bench.py --gpus N --shared-gpu` starts N ranks (torchrun, as for
+    N GPUs) that all trace on GPU 0; their tiles reach rank 0 as host copies
+    over gloo into mm_assemble_rows (mirror_maze.comm.HostComm: RCCL allows one
+    rank per GPU) -- everything else is the N-GPU run: the interleaved row
+    sets, NativeGatherer's slots and events, the rank >= 1 branches, the
+    exposed-gather clock and the reductions.  Rank 0's saved frame must equal
+    the texture-write conversion of trace_tile's last frame byte for byte, the
+    ranks' rays must add up to the 1-GPU frames' rays, and n_gpus is N."""
+    import json
+
+    from bench import CONFIGS
+    from mirror_maze import Renderer, Scene, default_uniform, make_ext
+
+    out = tmp_path / "frame.npy"
+    steps = 3
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", str(n_ranks), "--shared-gpu", "--config", "c2",
+           "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--save-frame", str(out)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == n_ranks and "diagnostics" in line["config"]["parallelism"]
+    d = line["distributed"]
+    assert d["shared_gpu"] is True and d["torch_distributed_world"] == n_ranks and d["rccl_world"] is None
+    assert "HostComm" in d["backend"] and d["gathers_total"] >= 1
+    k = d["kernel_ms_per_rank"]
+    assert 0 < k["min"] <= k["max"]
+    assert line["roofline"]["frac"] is None  # diagnostics: no roofline
+    maze_n, W, H, spp, bl, ml, _ = CONFIGS["c2"]
+    r = Renderer(0)
+    r.upload_scene(Scene.build(maze_n, 0))
+    u = default_uniform(W, H, 0)
+    rays = 0
+    for f in range(steps):
+        img, st = r.trace_tile(u, make_ext(spp, bl, ml, frame=f), 0, 0, W, H, stats=True)
+        rays += st.rays
+    assert line["config"]["rays_total"] == rays
+    got = np.load(out)
+    assert got.dtype == np.uint8 and got.shape == (H, W, 4)
+    assert np.array_equal(got, r.quantize(img).cpu().numpy())
+    r.close()
