@@ -423,8 +423,14 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
         // budget, else plain 32-bit words at the same cell size, before
         // coarser cells (the kernel variant for wide words stages all of it)
         if (wide && build_lists(rects, n_rects, recs, smin, smax, C, s, true, merge_axes, g, why)) {
-            if (maze_form(g)) compact_layout(g);
-            if (g.bytes <= index_budget) break;
+            const bool mf = maze_form(g);
+            if (mf) compact_layout(g);
+            // the maze forms' walk decodes face ranges only (no whole-list cells, mm_grid.h): a maze grid
+            // with a cell of more than 7 entries takes plain words
+            bool whole = false;
+            for (size_t c = 0; mf && c < (size_t)g.n[0] * g.n[1] * g.n[2]; ++c)
+                whole |= (g.image[8 * c + 7] & 0x80u) != 0;
+            if (g.bytes <= index_budget && !whole) break;
         }
         if (build_lists(rects, n_rects, recs, smin, smax, C, s, false, merge_axes, g, why) &&
             g.off_recs <= index_budget)
@@ -433,6 +439,18 @@ bool build_grid(const mm_rect* rects, uint32_t n_rects, const mm_node* nodes, ui
     }
     g.n_slow = n_slow_g;
     g.flat_ok = maze_form(g);
+    if (g.wide && g.flat_ok) {
+        // The maze forms never step y, so their x-entry faces' ranges move into the y faces' slots:
+        // +x -> bits 37-42, -x -> 43-48, beside +z / -z at 49-54 / 55-60 -- every range the walk reads
+        // is then in the word's high half (one 32-bit shift, mm_grid.h grid_search)
+        for (size_t c = 0; c < (size_t)g.n[0] * g.n[1] * g.n[2]; ++c) {
+            uint64_t w;
+            std::memcpy(&w, &g.image[8 * c], 8);
+            const uint64_t xf = (w >> 25) & 0xFFFull;
+            w = (w & ~(0xFFFull << 37)) | (xf << 37);
+            std::memcpy(&g.image[8 * c], &w, 8);
+        }
+    }
     g.slab = false;
     if (g.n_glob == 2) {
         const uint32_t m0 = grecs[8 * (size_t)g.glob[0] + 7], m1 = grecs[8 * (size_t)g.glob[1] + 7];

@@ -428,7 +428,20 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     uint32_t j, jend;
     auto cell_pos = [&](uint32_t sh) {
         constexpr bool kB = decltype(gv.list)::kStep == 2u;
-        if constexpr (kWide) {
+        if constexpr (kWide && kFlat) {
+            // maze forms (grid_build.cpp): no whole-list cells, and the x / z entry faces' ranges in the high
+            // half at bits 5 + 6 f' (f' = 0 +x, 1 -x, 2 +z, 3 -z): sh is that shift within the high half
+            const uint64_t cw = gv.cells.at64(cp);
+            const uint32_t lo = (uint32_t)cw, first = lo & 0x3FFFFFu;
+            if (sh == 0u) {  // the whole list (the first cell)
+                j = first;
+                jend = first + (kB ? (lo >> 21) & 0xEu : (lo >> 22) & 7u);
+            } else {
+                const uint32_t f = (uint32_t)(cw >> 32) >> sh;
+                j = first + (kB ? (twice(f) & 14u) : (f & 7u));
+                jend = j + (kB ? ((f >> 2) & 14u) : ((f >> 3) & 7u));
+            }
+        } else if constexpr (kWide) {
             const uint64_t cw = gv.cells.at64(cp);
             const uint32_t lo = (uint32_t)cw;
             const bool whole = (int32_t)(uint32_t)(cw >> 32) < 0;
@@ -451,47 +464,90 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     };
     cell_pos(0u);
     uint32_t cells = 1, tests = g.n_glob;
-    // Per cell: test the rects of its list, then step to the next cell (or
-    // stop).  (The compiler nests the tests in a per-cell loop either way;
-    // written as a do-while under one entry check, the loop carries one
-    // compare per test instead of a header and a latch compare.)
-    for (;;) {
-        MM_LANE_STAT(kLpGridIter);
-        if (j < jend) {
-            do {
-                MM_LANE_STAT(kLpRectTest);
-                grid_rect<kSlow, kFlat, kFlat>(gv, geo, gv.list.at(j), r, best, bk, tie);
-                j += gv.list.kStep;
-                if (kStats) ++tests;
-            } while (j < jend);
-        }
-        {
+    if constexpr (kFlat) {
+        // The maze forms' walk (one cell along y: the steps are x or z).  Every way
+        // out of the grid is folded into one end time per ray, tend = min(ty, the
+        // crossing time of the last x boundary, of the last z boundary) -- each
+        // computed with the same fma as the step that would cross it, from the
+        // same float boundary index, so a step reaches it exactly -- and the walk
+        // continues while min(tx, tz) <= best and < tend: no per-step bounds
+        // checks, no y-step test, no boundary-index conversion.  Against the 3-D
+        // walk below this skips only cells entered exactly at the end time (a tie
+        // of tx or tz with the exit, where that walk steps into a cell and leaves
+        // the grid in the same instant): such a cell meets the ray in one point,
+        // which lies on the face of the cell just tested, so the lists' eps
+        // covers it (header) and the answer is unchanged.  (CPU replay of every
+        // query of a C3 frame: scripts/grid_sim.c TEND=1.)
+        const float sgx = r.y.x > 0.0f ? 1.0f : -1.0f, sgz = r.y.z > 0.0f ? 1.0f : -1.0f;
+        float fbx = (float)bx, fbz = (float)bz;  // (exact small integers)
+        const float tend = fminf(ty, fminf(__builtin_fmaf(r.y.x > 0.0f ? (float)g.n[0] : 0.0f, Bx, Ax),
+                                           __builtin_fmaf(r.y.z > 0.0f ? (float)g.n[2] : 0.0f, Bz, Az)));
+        // (the high-half shifts of the +x / -x / +z / -z ranges: cell_pos, grid_build.cpp)
+        const uint32_t shx = kWide ? (r.y.x > 0.0f ? 5u : 11u) : 0u, shz = kWide ? (r.y.z > 0.0f ? 17u : 23u) : 0u;
+        for (;;) {
+            MM_LANE_STAT(kLpGridIter);
+            if (j < jend) {
+                do {
+                    MM_LANE_STAT(kLpRectTest);
+                    grid_rect<kSlow, kFlat, kFlat>(gv, geo, gv.list.at(j), r, best, bk, tie);
+                    j += gv.list.kStep;
+                    if (kStats) ++tests;
+                } while (j < jend);
+            }
             MM_LANE_STAT(kLpCellStep);
-            const float te = fminf(tx, fminf(ty, tz));
-            if (best < te) break;
-            // step the axis whose boundary comes first (x before y before z on
-            // equal times) -- in selects: three exec-mask branches here cost
-            // more SALU and SGPR spills than the selects cost VALU
-            const bool sx = tx == te, sy = !sx && ty == te, sz = !sx && !sy;
-            if (kFlat && sy) break;  // (one cell along y: the walk leaves the grid)
-            bx += sx ? (r.y.x > 0.0f ? 1 : -1) : 0;
-            by += sy ? (r.y.y > 0.0f ? 1 : -1) : 0;
-            bz += sz ? (r.y.z > 0.0f ? 1 : -1) : 0;
-            // (kFlat: by never moves from 0 / 1 and n[1] == 1)
-            if (((uint32_t)bx > (uint32_t)g.n[0]) | (!kFlat && (uint32_t)by > (uint32_t)g.n[1]) |
-                ((uint32_t)bz > (uint32_t)g.n[2]))
-                break;
-            // grid_time of the stepped axis, the same operations on selected operands
-            // (by-value selects: a select of two loads becomes a load of a
-            // selected address -- of the kernel argument or a scratch copy)
-            const int b = sx ? bx : (sy ? by : bz);
-            const float nt = __builtin_fmaf((float)b, sel_xy(sx, sy, F3{Bx, By, Bz}), sel_xy(sx, sy, F3{Ax, Ay, Az}));
-            tx = sx ? nt : tx;
-            ty = sy ? nt : ty;
-            tz = sz ? nt : tz;
-            cp += (uint32_t)(sx ? dcx : (sy ? dcy : dcz));
-            cell_pos((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu);
+            const bool sx = tx <= tz;  // (x before z on equal times)
+            const float te = sx ? tx : tz;  // (a select: fminf of selected values costs two canonicalising maxes)
+            if (!(te <= best) | !(te < tend)) break;
+            fbx = sx ? fbx + sgx : fbx;
+            fbz = sx ? fbz : fbz + sgz;
+            tx = sx ? __builtin_fmaf(fbx, Bx, Ax) : tx;
+            tz = sx ? tz : __builtin_fmaf(fbz, Bz, Az);
+            cp += (uint32_t)(sx ? dcx : dcz);
+            cell_pos(sx ? shx : shz);
             if (kStats) ++cells;
+        }
+    } else {
+        // Per cell: test the rects of its list, then step to the next cell (or
+        // stop).  (The compiler nests the tests in a per-cell loop either way;
+        // written as a do-while under one entry check, the loop carries one
+        // compare per test instead of a header and a latch compare.)
+        for (;;) {
+            MM_LANE_STAT(kLpGridIter);
+            if (j < jend) {
+                do {
+                    MM_LANE_STAT(kLpRectTest);
+                    grid_rect<kSlow, kFlat, kFlat>(gv, geo, gv.list.at(j), r, best, bk, tie);
+                    j += gv.list.kStep;
+                    if (kStats) ++tests;
+                } while (j < jend);
+            }
+            {
+                MM_LANE_STAT(kLpCellStep);
+                const float te = fminf(tx, fminf(ty, tz));
+                if (best < te) break;
+                // step the axis whose boundary comes first (x before y before z on
+                // equal times) -- in selects: three exec-mask branches here cost
+                // more SALU and SGPR spills than the selects cost VALU
+                const bool sx = tx == te, sy = !sx && ty == te, sz = !sx && !sy;
+                bx += sx ? (r.y.x > 0.0f ? 1 : -1) : 0;
+                by += sy ? (r.y.y > 0.0f ? 1 : -1) : 0;
+                bz += sz ? (r.y.z > 0.0f ? 1 : -1) : 0;
+                if (((uint32_t)bx > (uint32_t)g.n[0]) | ((uint32_t)by > (uint32_t)g.n[1]) |
+                    ((uint32_t)bz > (uint32_t)g.n[2]))
+                    break;
+                // grid_time of the stepped axis, the same operations on selected operands
+                // (by-value selects: a select of two loads becomes a load of a
+                // selected address -- of the kernel argument or a scratch copy)
+                const int b = sx ? bx : (sy ? by : bz);
+                const float nt = __builtin_fmaf((float)b, sel_xy(sx, sy, F3{Bx, By, Bz}),
+                                                sel_xy(sx, sy, F3{Ax, Ay, Az}));
+                tx = sx ? nt : tx;
+                ty = sy ? nt : ty;
+                tz = sz ? nt : tz;
+                cp += (uint32_t)(sx ? dcx : (sy ? dcy : dcz));
+                cell_pos((fsh >> (sx ? 0u : (sy ? 8u : 16u))) & 0xFFu);
+                if (kStats) ++cells;
+            }
         }
     }
     if (kStats) {

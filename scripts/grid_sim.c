@@ -159,7 +159,7 @@ static void build_grid(double cell_target) {
    every entry the neighbour across that face does not list */
 static uint32_t *fr_off, *fr_list;
 static uint8_t (*fr_s)[6], (*fr_l)[6];
-static int fr_on, start_on, direct_on;
+static int fr_on, start_on, direct_on, tend_on;
 static float start_t = 0.09375f;
 static int listed_in(long c, uint32_t k) {
     for (uint32_t q = cell_off[c]; q < cell_off[c + 1]; ++q) if (cell_list[q] == k) return 1;
@@ -169,6 +169,10 @@ static void build_faces(void) {
     fr_on = getenv("FACES") != NULL;
     start_on = getenv("START") != NULL;
     direct_on = getenv("DIRECT") != NULL;
+    /* TEND=1: the maze forms' walk (mm_grid.h, round 6): every exit folded into one end time per ray, the
+       minimum over axes of the last boundary's crossing time (the same cell_time form), the walk stopping once
+       the next crossing is not before it -- cells entered exactly at the exit instant are not visited */
+    tend_on = getenv("TEND") != NULL;
     /* START=1 (or 0): the kernel's t = 3/32; START=<t>: that t */
     if (start_on) { start_t = (float)atof(getenv("START")); if (!(start_t > 0.0f) || start_t == 1.0f) start_t = 0.09375f; }
     long total = (long)gn[0] * gn[1] * gn[2];
@@ -287,6 +291,12 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
         stp[a] = dd[a] > 0.0f ? 1 : -1;
         tn[a] = cell_time(a, i + (stp[a] > 0), oo[a], yy[a]);
     }
+    float tend = BIG;
+    if (tend_on)
+        for (int a = 0; a < 3; ++a) {
+            const float te_a = cell_time(a, stp[a] > 0 ? gn[a] : 0, oo[a], yy[a]);
+            if (te_a < tend) tend = te_a;
+        }
     int ncell = 0;
     q_n = 0;
     q_cell0 = (ic[2] * gn[1] + ic[1]) * gn[0] + ic[0];
@@ -317,6 +327,7 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
         int a = tn[0] <= tn[1] ? (tn[0] <= tn[2] ? 0 : 2) : (tn[1] <= tn[2] ? 1 : 2);
         prev_c = c;
         if (best < tn[a]) break;
+        if (tend_on && !(tn[a] < tend)) break;
         ic[a] += stp[a];
         face = 2 * a + (stp[a] > 0 ? 0 : 1);  /* entered through the face toward the previous cell */
         if (ic[a] < 0 || ic[a] >= gn[a]) break;
