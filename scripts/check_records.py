@@ -5,7 +5,7 @@ results directory with the source hash it carries against
 
     python scripts/check_records.py [--round r04]
 Exit status 1 when a top-level PMC record is stale (bench.py would then label
-its lines "stale" and fall back to the reference-walk model).
+its lines "stale" and print a null roofline fraction).
 """
 from __future__ import annotations
 
