@@ -105,6 +105,7 @@ struct DevGrid {
     // walk clamps a cell index instead of keeping a computed n - 1 live (the
     // compiler spills those to VGPR lanes: a single-slot v_readlane per use)
     int nm1[3];
+    float nf[3];               // n[a] as a float (the maze forms' end time: a kernel argument, not a hoisted convert)
 };
 
 struct DevScene {

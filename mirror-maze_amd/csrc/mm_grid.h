@@ -480,8 +480,8 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
         // query of a C3 frame: scripts/grid_sim.c TEND=1.)
         const float sgx = r.y.x > 0.0f ? 1.0f : -1.0f, sgz = r.y.z > 0.0f ? 1.0f : -1.0f;
         float fbx = (float)bx, fbz = (float)bz;  // (exact small integers)
-        const float tend = fminf(ty, fminf(__builtin_fmaf(r.y.x > 0.0f ? (float)g.n[0] : 0.0f, Bx, Ax),
-                                           __builtin_fmaf(r.y.z > 0.0f ? (float)g.n[2] : 0.0f, Bz, Az)));
+        const float tend = fminf(ty, fminf(__builtin_fmaf(r.y.x > 0.0f ? g.nf[0] : 0.0f, Bx, Ax),
+                                           __builtin_fmaf(r.y.z > 0.0f ? g.nf[2] : 0.0f, Bz, Az)));
         // (the high-half shifts of the +x / -x / +z / -z ranges: cell_pos, grid_build.cpp)
         const uint32_t shx = kWide ? (r.y.x > 0.0f ? 5u : 11u) : 0u, shz = kWide ? (r.y.z > 0.0f ? 17u : 23u) : 0u;
         for (;;) {
@@ -561,8 +561,11 @@ __device__ __forceinline__ bool grid_search(const DevGrid& g, const GV& gv, cons
     if (tie) return false;
     MM_LANE_STAT(kLpCert);
     // certificate: R*'s reference leaf box passes at every t > best
+    // (compact grids: the box of rect k = e / 8 at byte 24 k = 3 e, two pairable adds)
+    const float2* bp = kFlat ? reinterpret_cast<const float2*>(reinterpret_cast<const char*>(gv.box) + (bk + twice(bk)))
+                             : gv.box + 3 * bk;
     bk = rect_index<kFlat>(bk);
-    const float2 bxx = gv.box[3 * bk + 0], byy = gv.box[3 * bk + 1], bzz = gv.box[3 * bk + 2];
+    const float2 bxx = bp[0], byy = bp[1], bzz = bp[2];
     const float tx1 = qdiv(bxx.x - r.o.x, r.d.x, r.y.x), tx2 = qdiv(bxx.y - r.o.x, r.d.x, r.y.x);
     float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
     const float ty1 = qdiv(byy.x - r.o.y, r.d.y, r.y.y), ty2 = qdiv(byy.y - r.o.y, r.d.y, r.y.y);

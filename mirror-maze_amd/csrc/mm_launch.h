@@ -19,7 +19,7 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
 
 // Deferred path states (mirror-tail deferral): one 64-byte record per entry
 // (rec[4*i .. 4*i+3] = ori.xyz dir.x | dir.yz T.xy | T.z L.xyz | seed,
-// n | mh << 16, sample slot, 0 -- one base pointer; 15 SoA field arrays would
+// (n - mh) | mh << 15 | bank << 30, sample slot, s1 -- one base pointer; 16 SoA field arrays would
 // hold 15 addresses in SGPRs across the bounce loop), `cap` records; resident
 // block b owns the kTailRing records from b * kTailRing (its tail ring, at most
 // 2 blocks per CU).

@@ -573,7 +573,10 @@ int mm_upload_scene(mm_ctx* c, const mm_rect* rects, uint32_t n_rects, const mm_
         dg.slab = gh.slab ? 1u : 0u;
         dg.slab_y[0] = gh.slab_y[0];
         dg.slab_y[1] = gh.slab_y[1];
-        for (int a = 0; a < 3; ++a) dg.nm1[a] = gh.n[a] - 1;
+        for (int a = 0; a < 3; ++a) {
+            dg.nm1[a] = gh.n[a] - 1;
+            dg.nf[a] = (float)gh.n[a];
+        }
         for (int i = 0; i < 4; ++i) dg.glob[i] = gh.glob[i];
         dg.cells = c->d_grid;
         dg.list = reinterpret_cast<const uint16_t*>(c->d_grid + gh.off_list);

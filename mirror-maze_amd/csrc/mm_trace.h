@@ -453,14 +453,16 @@ __device__ __forceinline__ bool closest_hit_bvh(const DevScene& sc, const V& v, 
     }
 }
 
-// Path state carried across bounces.  bank = 1: the rejection-sampling trial
-// last drawn from the RNG (its three numbers end at `seed`) was accepted and
-// is the direction sample of the path's next diffuse bounce (shade_step).
+// Path state carried across bounces.  bank (0..2): accepted rejection-sampling
+// trials already drawn from the RNG for the path's next diffuse bounces
+// (shade_step): with bank >= 1 the first ends at s1 (its three numbers are the
+// three draws before state s1), with bank = 2 the second ends at `seed`; with
+// bank = 1 `seed` may lie past s1 by rejected trials only.
 struct PathState {
     F3 ori, dir, T, L;
     uint32_t seed;
     int n, mh;
-    uint32_t bank;
+    uint32_t bank, s1;
 };
 
 // random()'s state step s -> a s + c (shaders.metal:181-186, rand_pm1), and the
@@ -480,14 +482,23 @@ static_assert(kLcgBack3A * (((kLcgA * 12345u + kLcgC) * kLcgA + kLcgC) * kLcgA +
 
 // One shading step after a closest-hit query (the body of shaders.metal:306-340
 // after line 307).  Returns false when the path terminates.
+// A terminating path (a miss, shaders.metal:336-338, or a mirror bounce past
+// the limit, 326 / 333) keeps its L, the one field read after the bounce loop,
+// and runs the rest of the step on rect 0 as a mirror bounce with its results
+// discarded: every field but L is then dead, so the step writes the state
+// unconditionally and the bounce loop carries one copy of it (with early
+// returns the old and the new state were live together and the compiler copied
+// the whole state between register sets twice per bounce).
 __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, float t, uint32_t k, int mirror_limit) {
-    if (!(t < kBig)) return false;                           // miss, shaders.metal:336-338
+    const bool hit = t < kBig;
+    k = hit ? k : 0u;
     MM_LANE_STAT(kLpShade);
     const F3 nn = xyz(sc.geo[4 * k + 1]);                    // normalize(cross(v,u)), %238
     const float4 s0 = sc.shade[2 * k + 0];                   // color, is_mirror
     const float sg = msign(dot3(p.dir, nn));
-    const bool diffuse = s0.w == 0.0f || sg == 1.0f;
-    if (!diffuse && !(p.mh + 1 < mirror_limit)) return false;  // shaders.metal:326, 333
+    const bool lit = s0.w == 0.0f || sg == 1.0f;
+    const bool more = hit & (lit | (p.mh + 1 < mirror_limit));
+    const bool diffuse = more & lit;
     // Both branches end in ori += t dir, dir = normalize(X), L = contrib + L;
     // those run once after the branch (a wave holding diffuse and mirror lanes
     // would otherwise execute the correctly rounded 1/sqrt of each branch).
@@ -502,40 +513,48 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
         // for every binary32 x (exhaustive check: scripts/verify_sqrt_gt1.c).
         // The path's direction samples are its RNG stream's accepted trials in
         // order -- nothing else draws from it after the primary jitter -- so a
-        // lane may draw ahead.  The first trial: the banked one (its draws
-        // rewound and redrawn: the same numbers, the state ends where it was),
-        // else a fresh one.  Lanes whose trial is rejected loop; while they do,
-        // the wave's other diffuse lanes draw their NEXT bounce's trials until
-        // one is accepted (the bank), so that bounce's first trial is accepted
-        // on those lanes and the wave's loop runs for fewer lanes -- a wave runs
-        // its unluckiest lane's trials (~5.8 iterations per bounce on C3 where a
-        // lane needs 0.9).  (A wave-pooled form -- trials spread over the lanes
-        // with jumps of the state -- was bit-exact and slower: 12 % on C3 in
-        // round 2, 3.5 % in round 3, profiles/r03/ab_pool_trials.txt.)
-        uint32_t s = p.seed;
+        // lane may draw ahead, and may skip rejected trials it already drew.
+        // The first trial: the first banked one (its draws rewound from s1 and
+        // redrawn: the same numbers; the stream goes on from `seed`, past any
+        // rejected trials after it), else a fresh one.  Lanes whose trial is
+        // rejected loop; while they do, the wave's other diffuse lanes draw
+        // their NEXT bounces' trials until two are accepted (the bank), so those
+        // bounces' first trials are accepted on those lanes and the wave's loop
+        // runs for fewer lanes -- a wave runs its unluckiest lane's trials (~5.8
+        // iterations per bounce on C3 where a lane needs 0.9; a CPU model of 64
+        // lanes: 3.3 with a bank of one, 2.6 with two).  (A wave-pooled form --
+        // trials spread over the lanes with jumps of the state -- was bit-exact
+        // and slower: 12 % on C3 in round 2, 3.5 % in round 3,
+        // profiles/r03/ab_pool_trials.txt.)
+        uint32_t s = p.bank ? p.s1 : p.seed;
         if (p.bank) s = s * kLcgBack3A + kLcgBack3C;
         float rx = rand_pm1(s), ry = rand_pm1(s), rz = rand_pm1(s);
-        p.seed = s;
+        p.seed = p.bank ? p.seed : s;
+        p.s1 = p.seed;  // (the second banked trial, if any, ends there: it is the first now)
+        uint32_t bank = p.bank ? p.bank - 1u : 0u;
         F3 rd = F3{rx, ry, rz};
         float len2 = dot3(rd, rd);
-        uint32_t need = len2 > 0x1.000002p0f ? 1u : 0u, bank = 0u;
+        uint32_t need = len2 > 0x1.000002p0f ? 1u : 0u;
         if (__builtin_amdgcn_ballot_w64(need != 0u)) do {  // (do-while: no copies of the carried values)
             MM_LANE_STAT(kLpTrial);
-            // every lane draws (no branch: the loop is one block); a lane already
-            // holding a banked trial keeps its state (need = 1 implies bank = 0)
+            // every lane draws (no branch: the loop is one block); a lane whose
+            // bank is full keeps its state (need = 1 implies bank = 0)
             uint32_t t = p.seed;
             rx = rand_pm1(t); ry = rand_pm1(t); rz = rand_pm1(t);
             const float q2 = dot3(F3{rx, ry, rz}, F3{rx, ry, rz});
             // accepted <=> !(q2 > 1 + 2^-23) <=> q2 < 1 + 2^-22 <=> the sign of the exact difference
             // (q2 is finite) -- two pairable ops instead of a compare and a select
             const uint32_t acc = __float_as_uint(q2 - 0x1.000004p0f) >> 31;
-            p.seed = bank ? p.seed : t;
+            const uint32_t act = (bank >> 1) ^ 1u;  // bank < 2: still drawing
+            p.seed = act ? t : p.seed;
             const uint32_t take = need & acc;
             rd.x = take ? rx : rd.x;
             rd.y = take ? ry : rd.y;
             rd.z = take ? rz : rd.z;
             len2 = take ? q2 : len2;
-            bank |= acc - take;  // accepted on a lane that did not need it
+            const uint32_t gain = (acc & act) - take;  // accepted on a lane that did not need it
+            p.s1 = gain > bank ? t : p.s1;              // the first banked trial's end
+            bank += gain;
             need -= take;
         } while (__builtin_amdgcn_ballot_w64(need != 0u));
         p.bank = bank;
@@ -550,8 +569,9 @@ __device__ __forceinline__ bool shade_step(const DevScene& sc, PathState& p, flo
     }
     p.ori = p.ori + t * p.dir;                               // %363
     p.dir = rsq(dot3(x, x)) * x;                             // %372 / reflect's normalize
-    p.L = contrib + p.L;                                     // %409
-    return true;
+    const F3 l = contrib + p.L;                              // %409
+    p.L = F3{more ? l.x : p.L.x, more ? l.y : p.L.y, more ? l.z : p.L.z};
+    return more;
 }
 
 }  // namespace mm

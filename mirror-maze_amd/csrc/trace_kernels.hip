@@ -154,7 +154,7 @@ __global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, f
 // resolve).
 
 // A deferred path's state (64 B: ori.xyz dir.x | dir.yz T.xy | T.z L.xyz |
-// seed, n | mh << 16, sample slot, bank) into / out of slot s of its block's tail
+// seed, (n - mh) | mh << 15 | bank << 30, sample slot, s1) into / out of slot s of its block's tail
 // ring.  kLdsPay (the deferral kernel with kRing = 2, chosen where the grid
 // image leaves room -- C3: 44 KB image + 34 KB static LDS per block, two
 // blocks per CU): the payload lives in the block's LDS beside the turn words,
@@ -175,7 +175,9 @@ __device__ __forceinline__ void tail_store(const TailQueue& q, uint32_t s, const
                                 __float_as_uint(p.T.y));
     const uint4 w2 = make_uint4(__float_as_uint(p.T.z), __float_as_uint(p.L.x), __float_as_uint(p.L.y),
                                 __float_as_uint(p.L.z));
-    const uint4 w3 = make_uint4(p.seed, (uint32_t)p.n | ((uint32_t)p.mh << 16), slot, p.bank);
+    // (mh <= n and n - mh < bounce_limit <= 32767, mh < mirror_limit <= 32767: mm_runtime.hip checks the limits)
+    const uint32_t nmb = (uint32_t)(p.n - p.mh) | ((uint32_t)p.mh << 15) | (p.bank << 30);
+    const uint4 w3 = make_uint4(p.seed, nmb, slot, p.s1);
     if constexpr (kLdsPay) {
         uint4* r = ring_pay() + s;
         r[0] = w0; r[kTailRing] = w1; r[2 * kTailRing] = w2; r[3 * kTailRing] = w3;
@@ -200,9 +202,10 @@ __device__ __forceinline__ uint32_t tail_load(const TailQueue& q, uint32_t s, Pa
     p.T = F3{__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x)};
     p.L = F3{__uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w)};
     p.seed = d.x;
-    p.n = (int)(d.y & 0xFFFFu);
-    p.mh = (int)(d.y >> 16);
-    p.bank = d.w;
+    p.mh = (int)((d.y >> 15) & 0x7FFFu);
+    p.n = (int)(d.y & 0x7FFFu) + p.mh;
+    p.bank = d.y >> 30;
+    p.s1 = d.w;
     return d.z;
 }
 
@@ -492,6 +495,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             p.n = 0;
             p.mh = 0;
             p.bank = 0u;
+            p.s1 = 0u;
             bool overflow = false;
             bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow);
             if (overflow) atomicOr(err, kErrStack);
