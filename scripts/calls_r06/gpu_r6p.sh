@@ -1,0 +1,16 @@
+# round 6, call p: C5 as BASELINE.json states it (120 accumulated frames), rocprofv3 --stats of C2 / C4 /
+# C5-120, and the emulated per-rank scaling (rank 0's rows of an N-way split on one GPU, N = 1, 2, 4, 8)
+set -o pipefail
+mkdir -p gpurun_out/r6finres2
+timeout -k 10 300 python bench.py --config c5 --accumulate --steps 120 --warmup 1 --no-cpu-baseline \
+  > gpurun_out/r6finres2/c5_acc120.json 2> gpurun_out/r6finres2/c5_acc120.err || exit $?
+export TMPDIR=/tmp; mkdir -p gpurun_out/r6prof2
+for C in "c2|--config c2 --steps 10 --warmup 2" "c4|--config c4 --steps 4 --warmup 1" \
+         "c5_acc120|--config c5 --accumulate --steps 120 --warmup 1"; do
+  n=${C%%|*}; a=${C#*|}
+  ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/gpurun_out/r6prof2/$n \
+      -o run -- python3 $GRAFT_REPO_ROOT/bench.py $a --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/r6prof2/$n.log 2>&1 ) \
+    || { echo "rocprof $n failed"; exit 1; }
+done
+bash scripts/emulated_scaling.sh r6emu2 || exit $?
+echo r6p done
