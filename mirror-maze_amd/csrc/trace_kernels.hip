@@ -317,7 +317,7 @@ __device__ __forceinline__ uint32_t ring_claim(uint32_t need, uint32_t& first) {
 // The record (TileJob::ring_diag, host-mapped, 16 words; mm_last_error prints
 // it): [0] 1 = written, [1] role (1 reader, 2 writer), [2] entry seq, [3]
 // wanted turn value, [4] the turn value last seen, [5] reserved, [6] claimed,
-// [7] block, [8] wave, [9] lane, [10..11] 0, [12..13] wall clock at the
+// [7] block, [8] wave, [9] lane, [10..11] unused, [12..13] wall clock at the
 // timeout (100 MHz), [14] polls, [15] launch id.  (No clock at the wait's
 // start: a 64-bit value live across the wait loop cost the deferral kernel
 // 10 more scratch operations in its chunk loop; the polls give the length.)
@@ -337,7 +337,8 @@ __device__ __forceinline__ void ring_timeout(const TileJob& job, uint32_t* err, 
     d[1] = role; d[2] = seq; d[3] = want; d[4] = seen;
     d[5] = lds_ld(ring_ctl() + 0); d[6] = lds_ld(ring_ctl() + 1);
     d[7] = blockIdx.x; d[8] = threadIdx.x >> 6; d[9] = threadIdx.x & 63u;
-    d[10] = 0u; d[11] = 0u; d[12] = (uint32_t)t1; d[13] = (uint32_t)(t1 >> 32);
+    d[12] = (uint32_t)t1; d[13] = (uint32_t)(t1 >> 32);  // ([10..11] unwritten: two zero registers
+    // held for them across the kernel were spilled around every chunk's bounce loop -- 1 KB of scratch per chunk)
     d[14] = polls; d[15] = job.launch_id;
     __threadfence_system();
     __hip_atomic_store(d, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
