@@ -257,6 +257,33 @@ def test_camera_sweep(gpu, maze_n, bl, ml):
     r.close()
 
 
+@pytest.mark.parametrize("bl,ml", [(40, 40), (3, 200)], ids=["long-paths", "mirror-chains"])
+def test_long_paths_through_the_tail_rings(gpu, bl, ml):
+    """Paths parked in the tail rings and resumed carry their state in a 64-B
+    record: (n - mh) | mh << 15 | bank << 30 and the first banked trial's end
+    s1 (trace_kernels.hip tail_store).  Long paths (40 / 40 bounces) and long
+    mirror chains (mirror limit 200, so mh runs past what 8 bits hold) through
+    forced deferral, every pixel vs the oracle; the same frame with deferral
+    off too."""
+    from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(16)
+    u = default_uniform(160, 90, 0)
+    e = make_ext(8, bl, ml, frame=11)
+    ref, n = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 160, 90)
+    for opts in ({21: 32, 22: 0}, {21: 0}):
+        r = Renderer(0)
+        r.set_pipeline(MM_PIPE_AUTO)
+        for k, v in opts.items():
+            r.set_option(k, v)
+        r.upload_scene(s)
+        got, st = r.trace_tile(u, e, 0, 0, 160, 90, stats=True)
+        assert _diff(got.cpu().numpy(), ref) == 0, opts
+        assert st.rays == n
+        r.close()
+
+
 @pytest.mark.parametrize("case", ["c3-two-frames-rings", "c3-two-frames-fused", "c2-frame", "spp3-strided"])
 def test_rgba8_frames_equal_the_quantized_float_frames(gpu, case):
     """MM_EXT_RGBA8: the trace writes each pixel's texture-write conversion

@@ -467,7 +467,7 @@ def test_bench_issue_mode_calibration(gpu):
 @pytest.mark.gpu
 def test_trace_tile_rejects_limits_beyond_the_packed_state(gpu):
     """Bounce / mirror limits above 32767 would overflow the tail records'
-    bounces | mirror hits << 16 word: an error code, not a wrong image."""
+    (n - mh) | mh << 15 | bank << 30 word: an error code, not a wrong image."""
     from mirror_maze import Renderer, default_uniform, make_ext
     from mirror_maze._lib import MMError
 
