@@ -257,6 +257,8 @@ static inline void consider(float a, uint32_t k, float* best, uint32_t* bk, int*
 /* grid search + verification; returns 1 and (t, index) when certified */
 #define MAXC 128
 static __thread int q_len[MAXC];   /* list lengths of the cells the last query visited */
+static __thread int q_lx[MAXC];    /* ... of them x-normal (the axis-split model below) */
+static uint8_t* rect_xn;           /* rect k is x-normal */
 static __thread int q_n;
 static __thread int q_cell0, q_oct;  /* the last query's start cell and direction octant (DUMP) */
 /* crossing time of boundary b along axis a: the kernel's fma form (mm_grid.h,
@@ -313,7 +315,12 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
             if (face >= 0 && getenv("NOY") && (face >> 1) == 1) j1 = j0 + cell_off[c + 1] - cell_off[c];
             else if (face >= 0) { j0 += fr_s[c][face]; j1 += fr_s[c][face]; }
         }
-        if (ncell < MAXC) q_len[ncell] = (int)(j1 - j0);
+        if (ncell < MAXC) {
+            q_len[ncell] = (int)(j1 - j0);
+            int nx = 0;
+            for (uint32_t j = j0; j < j1; ++j) nx += rect_xn[L[j]];
+            q_lx[ncell] = nx;
+        }
         ncell++;
         q_n = ncell < MAXC ? ncell : MAXC;
         for (uint32_t j = j0; j < j1; ++j) {
@@ -355,7 +362,7 @@ static int grid_query(v3 o, v3 d, float* t_out, uint32_t* i_out, gstats* st) {
 
 /* wave model: per lane, per bounce, the list lengths of the visited cells */
 #define MAXB 32
-static __thread int w_len[64][MAXB][16], w_n[64][MAXB], w_nb[64], w_lane;
+static __thread int w_len[64][MAXB][16], w_lx[64][MAXB][16], w_n[64][MAXB], w_nb[64], w_lane;
 /* DUMP=<file>: one 16-byte record per query, in path order, for the regrouping
    model (scripts/regroup_model.cpp): path id, bounce, start cell, octant, cells
    visited, the list length of the first 8 cells, and the rejection-sampling
@@ -399,7 +406,7 @@ static v3 path(v3 ori, v3 dir, uint32_t seed, int bl, int ml, gstats* st, trav_t
         if (n >= bl) { st->tail_q++; st->tail_tests += st->tests - t_before; st->tail_cells += st->cells - c_before; }
         if (n < MAXB) {
             w_n[w_lane][n] = q_n < 16 ? q_n : 16;
-            for (int c = 0; c < w_n[w_lane][n]; ++c) w_len[w_lane][n][c] = q_len[c];
+            for (int c = 0; c < w_n[w_lane][n]; ++c) { w_len[w_lane][n][c] = q_len[c]; w_lx[w_lane][n][c] = q_lx[c]; }
             w_nb[w_lane] = n + 1;
         }
         if (ok_q) {
@@ -461,6 +468,11 @@ int main(int argc, char** argv) {
     build_grid(argc > 8 ? atof(argv[8]) : 0.0);
     if (getenv("DUMP")) dump_f = fopen(getenv("DUMP"), "wb");
     build_faces();
+    rect_xn = calloc(S.n_rects, 1);
+    for (uint32_t k = 0; k < S.n_rects; ++k) {
+        const v3 nn = cross3(ld3(S.rects[k].v), ld3(S.rects[k].u));
+        rect_xn[k] = fabsf(nn.x) > fabsf(nn.y) && fabsf(nn.x) > fabsf(nn.z);
+    }
     mm_uniform u;
     /* default camera (mm_uniform_default): centre (-5,0,-45), quat from (0.1,0,1), focal 1, viewport (2W/H, 2) */
     u.cam.center[0] = -5.0f; u.cam.center[1] = 0.0f; u.cam.center[2] = -45.0f; u.cam.focal = 1.0f;
@@ -471,6 +483,7 @@ int main(int argc, char** argv) {
     memset(&tot, 0, sizeof tot);
     double wnest = 0, wflat = 0, wlane = 0, wcont[4] = {0, 0, 0, 0}, wtest = 0, wstep = 0, wshade = 0;
     double gnbmax = 0, gnbsum = 0, gnbw = 0, gact[32] = {0}, git[32] = {0};
+    double gqmix = 0, gqsplit = 0, gitmix = 0, gitsplit = 0;
     uint64_t rays_tot = 0;
 #pragma omp parallel
     {
@@ -480,6 +493,7 @@ int main(int argc, char** argv) {
         uint64_t rays = 0;
         double nest = 0, flat = 0, lanework = 0, ideal = 0, lockS = 0, cont[4] = {0, 0, 0, 0}, ntest = 0, nstep = 0;
         double nbmax = 0, nbsum = 0, nbw = 0, act_hist[32] = {0}, it_hist[32] = {0};
+        double qmix = 0, qsplit = 0, itmix = 0, itsplit = 0;
 #pragma omp for schedule(dynamic, 1)
         for (int y = 0; y < H; y += rs)
             for (int x0 = 0; x0 < W; x0 += 64 / spp) {
@@ -511,10 +525,18 @@ int main(int argc, char** argv) {
                     }
                     if (!any) break;
                     for (int c = 0; c < maxc; ++c) {
-                        int mx = 0;
-                        for (int l = 0; l < 64; ++l) if (w_nb[l] > b && w_n[l][b] > c && w_len[l][b][c] > mx) mx = w_len[l][b][c];
+                        int mx = 0, mxx = 0, mxz = 0;
+                        for (int l = 0; l < 64; ++l) if (w_nb[l] > b && w_n[l][b] > c) {
+                            if (w_len[l][b][c] > mx) mx = w_len[l][b][c];
+                            if (w_lx[l][b][c] > mxx) mxx = w_lx[l][b][c];
+                            if (w_len[l][b][c] - w_lx[l][b][c] > mxz) mxz = w_len[l][b][c] - w_lx[l][b][c];
+                        }
                         nest += mx * 45.0 + 25.0;
                         ntest += mx * 45.0; nstep += 25.0;
+                        /* quad-cycles: one mixed test loop (12.5 per test) vs an x loop and a z loop
+                           without the axis selects (9.5 per test, 1.5 more per cell for the second loop) */
+                        qmix += mx * 12.5 + 12.0; qsplit += (mxx + mxz) * 9.5 + 13.5;
+                        itmix += mx; itsplit += mxx + mxz;
                     }
                     flat += maxflat * 70.0;
                     lockS += 250.0;
@@ -550,7 +572,8 @@ int main(int argc, char** argv) {
             }
         if (dump_f) dump_flush();
 #pragma omp critical
-        { wnest += nest + lockS; wflat += flat + lockS; wtest += ntest; wstep += nstep; wshade += lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K];
+        { gqmix += qmix; gqsplit += qsplit; gitmix += itmix; gitsplit += itsplit;
+          wnest += nest + lockS; wflat += flat + lockS; wtest += ntest; wstep += nstep; wshade += lockS; wlane += lanework; for (int K = 0; K < 4; ++K) wcont[K] += cont[K];
           gnbmax += nbmax; gnbsum += nbsum; gnbw += nbw; for (int b = 0; b < 32; ++b) { gact[b] += act_hist[b]; git[b] += it_hist[b]; } }
 #pragma omp critical
         {
@@ -572,6 +595,8 @@ int main(int argc, char** argv) {
     printf("wave model (VALU slots x64 per wave): nested %.4g  flat %.4g  ideal(lane work/64) %.4g  -> util nested %.3f flat %.3f\n",
            wnest, wflat, wlane / 64, wlane / 64 / wnest, wlane / 64 / wflat);
     printf("nested split: tests %.4g  cell steps %.4g  shading %.4g\n", wtest, wstep, wshade);
+    printf("axis-split model (lockstep waves): test wave-iterations mixed %.4g split %.4g (x %.3f); quad-cycles of tests + steps mixed %.4g split %.4g (x %.3f)\n",
+           gitmix, gitsplit, gitsplit / gitmix, gqmix, gqsplit, gqsplit / gqmix);
     printf("with shading (250/bounce): lockstep nested %.4g flat %.4g | continuous thr1 %.4g thr16 %.4g thr32 %.4g thr64 %.4g\n",
            wnest, wflat, wcont[0], wcont[1], wcont[2], wcont[3]);
     printf("per wave: mean of max queries/lane %.3f, mean queries/lane %.3f\n", gnbmax / gnbw, gnbsum / gnbw);
