@@ -134,7 +134,7 @@ int  mm_trace_tile(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext,
  * for frame sequences; a frame's result is only complete when the launch is).
  * Needs the wave-persistent kernel with the fused resolve (64 % spp == 0) or
  * with the mirror-tail deferral (any spp: samples staged per frame and
- * resolved in one pass, at most 2^29 staged paths = 8 GiB per launch; over
+ * resolved in one pass, at most 2^29 staged paths = 6 GiB per launch; over
  * that a fusable launch runs without deferral, others get MM_ERR_INVALID);
  * MM_EXT_ACCUMULATE is rejected (frames of one launch run concurrently). */
 int  mm_trace_tile_frames(mm_ctx* ctx, const mm_uniform* uni, const mm_ext* ext, uint32_t n_frames,

@@ -53,7 +53,7 @@ struct mm_ctx {
     uint32_t* d_chunks = nullptr;
     size_t chunks_cap = 0;
     // per-sample staging (throughput mode)
-    float4* d_samples = nullptr;
+    mm::Sample* d_samples = nullptr;
     size_t samples_cap = 0;
     // mirror-tail rings' records (MM_OPT_DEFER)
     void* d_tail = nullptr;

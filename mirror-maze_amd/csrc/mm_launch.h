@@ -17,6 +17,12 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
                                uint32_t grid_w, uint32_t grid_h, float4* fb, uint32_t* fb8,
                                unsigned long long* stats_dev, uint32_t* err, bool count_stats, hipStream_t s);
 
+// A staged sample: the path's value sqrt(max(L, 0)) (shaders.metal:342-344),
+// 12 B -- the resolve reads these back (round 6: 16-B float4 slots before, a
+// quarter of the staged traffic unused).
+using Sample = F3;
+static_assert(sizeof(Sample) == 12, "three floats, no padding");
+
 // Deferred path states (mirror-tail deferral): one 64-byte record per entry
 // (rec[4*i .. 4*i+3] = ori.xyz dir.x | dir.yz T.xy | T.z L.xyz | seed,
 // (n - mh) | mh << 15 | bank << 30, sample slot, s1 -- one base pointer; 16 SoA field arrays would
@@ -98,7 +104,7 @@ struct MegaOpts {
 
 // MM_PIPE_REFERENCE: one thread per (pixel, sample) path; writes
 // the per-sample value sqrt(max(L,0)) to samples[path] (path = pixel*spp+s).
-hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples,
+hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, Sample* samples,
                              unsigned long long* stats_dev, uint32_t* err, bool count_stats,
                              const MegaOpts& o, hipStream_t s);
 
@@ -107,7 +113,7 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
 // and are left zero by the kernel itself (the last wave re-zeroes them).
 // lds_mode / form: trace_kernels.hip (k_trace_wavepersist); returns
 // hipErrorInvalidValue for a pair that is not instantiated.
-hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
+hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, Sample* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s);
 size_t wavepersist_lds_bytes(const DevScene& sc, int lds_mode);
@@ -127,6 +133,6 @@ hipError_t launch_chunk_packets(const float4* fb, const uint32_t* chunks, uint32
 hipError_t launch_quantize(const float4* in, uint32_t* out, size_t n, hipStream_t s);
 
 // Per-pixel reduction of spp samples in the reference's order, then / spp.
-hipError_t launch_resolve(const TileJob& job, const float4* samples, void* out, hipStream_t s);
+hipError_t launch_resolve(const TileJob& job, const Sample* samples, void* out, hipStream_t s);
 
 }  // namespace mm

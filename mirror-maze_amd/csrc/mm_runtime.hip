@@ -34,7 +34,7 @@ constexpr uint32_t kStatusSlots = 1024;
 constexpr uint32_t kRingDiagWords = 16;  // after the status words: the first timed-out ring wait's record
 constexpr size_t kFailedKept = 64;
 // Staged samples (tail deferral / no fused resolve) per launch: whole rows up
-// to this many paths (16 B each: 8 GiB).  A multi-frame launch over the cap
+// to this many paths (12 B each: 6 GiB).  A multi-frame launch over the cap
 // runs without deferral (fused resolve) or is refused.
 constexpr uint64_t kStagePathsMax = 1ull << 29;
 
@@ -871,7 +871,7 @@ int trace_tile_impl(mm_ctx* c, const mm_uniform* u, const mm_ext* e, uint32_t n_
         if (queue + (1ull << 24) > 0xFFFFFFFFull)
             return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: more paths than one launch holds (2^32)");
         if (defer && tile_paths * n_frames > kStagePathsMax)
-            return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: the frames' staged samples exceed 8 GiB "
+            return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: the frames' staged samples exceed 6 GiB "
                                            "(2^29 paths) per launch; use fewer frames per launch");
         if (rows_per_batch < h) return fail(c, MM_ERR_INVALID, "mm_trace_tile_frames: tile too large for one launch");
     }

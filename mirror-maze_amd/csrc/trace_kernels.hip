@@ -106,7 +106,7 @@ hipError_t launch_trace_chunks(const DevScene& sc, const mm_uniform& u, const ui
 // removed in round 6)
 template <bool kStats, typename Q>
 __device__ __forceinline__ void mega_body(const DevScene& sc, const Q& q, const TileJob& job,
-                                          float4* __restrict__ samples, unsigned long long* stats, uint32_t* err) {
+                                          Sample* __restrict__ samples, unsigned long long* stats, uint32_t* err) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;
     const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;
@@ -123,13 +123,13 @@ __device__ __forceinline__ void mega_body(const DevScene& sc, const Q& q, const 
         const F3 s = trace_path<kStats>(sc, q, ori, d, seed, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack,
                                         c, overflow);
         if (overflow) atomicOr(err, 1u);
-        samples[path] = make_float4(s.x, s.y, s.z, 0.0f);
+        samples[path] = s;
     }
     if (kStats) flush_stats(stats, c, path < n_paths ? 1u : 0u);
 }
 
 template <bool kStats>
-__global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, float4* __restrict__ samples,
+__global__ __launch_bounds__(1024) void k_trace_mega(DevScene sc, TileJob job, Sample* __restrict__ samples,
                                                      unsigned long long* stats, uint32_t* err) {
     mega_body<kStats>(sc, RefQuery<kStats>{sc}, job, samples, stats, err);
 }
@@ -366,8 +366,8 @@ __device__ __forceinline__ bool ring_wait(uint32_t seq, uint32_t c, uint32_t rol
     }
 }
 
-__device__ __forceinline__ void poison(float4* samples, uint32_t slot, uint32_t n_slots) {
-    if (slot < n_slots) samples[slot] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.0f);
+__device__ __forceinline__ void poison(Sample* samples, uint32_t slot, uint32_t n_slots) {
+    if (slot < n_slots) samples[slot] = Sample{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
 }
 
 #ifndef MM_CLAIM_CHUNKS
@@ -458,7 +458,7 @@ __device__ __forceinline__ uint32_t dequeue(uint32_t* work, uint32_t n_queue) {
 
 template <bool kStats, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q& q, const TileJob& job,
-                                                     float4* __restrict__ samples, unsigned long long* stats,
+                                                     Sample* __restrict__ samples, unsigned long long* stats,
                                                      uint32_t* err, uint32_t* work) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;         // per frame
@@ -501,7 +501,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
             bounce_loop<kStats>(sc, q, p, (int)job.e.bounce_limit, (int)job.e.mirror_limit, stack, c, overflow);
             if (overflow) atomicOr(err, kErrStack);
             s = path_value(p);
-            if (!job.fuse) samples[fr * n_paths + path] = make_float4(s.x, s.y, s.z, 0.0f);
+            if (!job.fuse) samples[fr * n_paths + path] = s;
             paths++;
         }
         if (job.fuse) resolve_in_wave(job, s, path, valid, job.out, (size_t)fr * job.w * job.h);
@@ -539,7 +539,7 @@ __device__ __forceinline__ uint32_t wavepersist_body(const DevScene& sc, const Q
 // as a new one (and may defer again) -- one copy of the loop in the kernel.
 template <bool kStats, bool kLdsPay, typename Q>
 __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, const Q& q, const TileJob& job,
-                                              float4* __restrict__ samples, unsigned long long* stats, uint32_t* err,
+                                              Sample* __restrict__ samples, unsigned long long* stats, uint32_t* err,
                                               uint32_t* work) {
     const uint32_t spp = job.e.spp;
     const uint32_t n_paths = job.w * job.h * spp;
@@ -649,7 +649,7 @@ __device__ __forceinline__ uint32_t wavepersist_ring_body(const DevScene& sc, co
                 }
             } else {
                 const F3 s = path_value(p);
-                samples[slot] = make_float4(s.x, s.y, s.z, 0.0f);
+                samples[slot] = s;
                 paths++;
             }
         }
@@ -883,7 +883,7 @@ hipError_t launch_publish_status(uint32_t* err, uint32_t* status, hipStream_t s)
 constexpr uint32_t kWpThreads = MM_WP_THREADS;
 // kRing: 0 no tail deferral; 1 tail rings, payload in global records; 2 tail rings, payload in LDS.
 template <bool kStats, int kLds, int kForm, int kRing>
-__global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersist(DevScene sc, TileJob job, float4* __restrict__ samples,
+__global__ __launch_bounds__(MM_WP_THREADS, MM_WP_WAVES) void k_trace_wavepersist(DevScene sc, TileJob job, Sample* __restrict__ samples,
                                                                unsigned long long* stats, uint32_t* err,
                                                                uint32_t* work) {
     if constexpr (kRing != 0) {  // the block's tail ring: counters and turn words zero
@@ -944,7 +944,7 @@ static uint32_t persistent_grid(K kern, size_t lds, uint32_t reserve_cus, uint64
 }
 
 template <int kLds, int kForm, int kRing>
-static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, float4* samples,
+static hipError_t launch_wavepersist_t(const DevScene& sc, const TileJob& job, Sample* samples,
                                        unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                        hipStream_t s) {
     // modes 11 / 14 stage into the kernel's static grid array (stage_and_run): no dynamic LDS, and an image
@@ -997,7 +997,7 @@ bool wavepersist_defer_built(int lds_mode, int form) {
     return false;
 }
 
-hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, float4* samples,
+hipError_t launch_trace_wavepersist(const DevScene& sc, const TileJob& job, Sample* samples,
                                     unsigned long long* stats, uint32_t* err, uint32_t* work, bool count_stats,
                                     int lds_mode, int form, hipStream_t s) {
     const int ring = job.defer_from < (1u << 30) ? (job.ring_lds ? 2 : 1) : 0;
@@ -1032,7 +1032,7 @@ hipError_t wavepersist_attributes(int lds_mode, int form, int ring, hipFuncAttri
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* samples, unsigned long long* stats_dev,
+hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, Sample* samples, unsigned long long* stats_dev,
                              uint32_t* err, bool count_stats, const MegaOpts& o, hipStream_t s) {
     if (!o.reference) return hipErrorInvalidValue;  // one thread per path: MM_PIPE_REFERENCE only
     const uint32_t n = job.w * job.h * job.e.spp;
@@ -1047,22 +1047,22 @@ hipError_t launch_trace_mega(const DevScene& sc, const TileJob& job, float4* sam
 // ---------------------------------------------------------------------------
 // Sample reduction: spp % 8 == 0 -> pairwise tree in blocks of 8, blocks added
 // left to right (the reference order for 64 spp); otherwise left to right.
-__global__ void k_resolve(TileJob job, const float4* __restrict__ samples, void* __restrict__ out) {
+__global__ void k_resolve(TileJob job, const Sample* __restrict__ samples, void* __restrict__ out) {
     const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= job.w * job.h) return;
     const uint32_t spp = job.e.spp;
-    const float4* s = samples + (size_t)pix * spp;
+    const Sample* s = samples + (size_t)pix * spp;
     F3 acc;
     if (spp % 8 == 0) {
         for (uint32_t b = 0; b < spp; b += 8) {
-            const F3 p0 = xyz(s[b + 0]) + xyz(s[b + 1]), p1 = xyz(s[b + 2]) + xyz(s[b + 3]);
-            const F3 p2 = xyz(s[b + 4]) + xyz(s[b + 5]), p3 = xyz(s[b + 6]) + xyz(s[b + 7]);
+            const F3 p0 = s[b + 0] + s[b + 1], p1 = s[b + 2] + s[b + 3];
+            const F3 p2 = s[b + 4] + s[b + 5], p3 = s[b + 6] + s[b + 7];
             const F3 blk = (p0 + p1) + (p2 + p3);
             acc = (b == 0) ? blk : acc + blk;
         }
     } else {
-        acc = xyz(s[0]);
-        for (uint32_t k = 1; k < spp; ++k) acc = acc + xyz(s[k]);
+        acc = s[0];
+        for (uint32_t k = 1; k < spp; ++k) acc = acc + s[k];
     }
     const float m = (float)spp;
     store_pixel(job, out, pix, F3{acc.x / m, acc.y / m, acc.z / m});
@@ -1071,16 +1071,16 @@ __global__ void k_resolve(TileJob job, const float4* __restrict__ samples, void*
 // The same reduction when 64 % spp == 0, a wave per 64 consecutive samples
 // (64/spp whole pixels): every load is one coalesced 1-KB wave access, and
 // resolve_in_wave adds in k_resolve's order (bit-identical).
-__global__ __launch_bounds__(256) void k_resolve_wave(TileJob job, const float4* __restrict__ samples,
+__global__ __launch_bounds__(256) void k_resolve_wave(TileJob job, const Sample* __restrict__ samples,
                                                       void* __restrict__ out) {
     const uint32_t n = job.w * job.h * job.e.spp;
     const uint32_t path = blockIdx.x * blockDim.x + threadIdx.x;  // waves never straddle the end: n % 64 == 0
     const bool valid = path < n;                                   // unless the tile is ragged
-    const float4 v = valid ? samples[path] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    resolve_in_wave(job, F3{v.x, v.y, v.z}, path, valid, out, 0);
+    const Sample v = valid ? samples[path] : Sample{0.0f, 0.0f, 0.0f};
+    resolve_in_wave(job, v, path, valid, out, 0);
 }
 
-hipError_t launch_resolve(const TileJob& job, const float4* samples, void* out, hipStream_t s) {
+hipError_t launch_resolve(const TileJob& job, const Sample* samples, void* out, hipStream_t s) {
     const uint32_t n = job.w * job.h;
     if (64 % job.e.spp == 0) {
         const uint32_t paths = n * job.e.spp;

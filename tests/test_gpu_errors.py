@@ -313,7 +313,7 @@ def test_status_of_calls_older_than_the_failed_list_is_not_reported_clean(gpu):
 
 
 def test_staging_bound_for_multi_frame_launches(gpu):
-    """staged samples are bounded at 2^29 paths (8 GiB) per launch.
+    """staged samples are bounded at 2^29 paths (6 GiB of 12-B records) per launch.
     A multi-frame launch over it runs with the fused resolve when it can
     (MM_INFO_LAST_DEFER 0, frames bit-identical to single-frame launches) and
     is refused otherwise; a single frame over it is split into row batches."""
