@@ -50,6 +50,17 @@ __device__ __forceinline__ void store_pixel(const TileJob& job, void* __restrict
     }
 }
 
+// The pixel's mean, sum / spp: when spp = 2^k as sum * 2^-k (both are the
+// exact sum x 2^-k rounded once: the same float, without three IEEE divisions).
+__device__ __forceinline__ F3 pixel_mean(F3 acc, uint32_t spp) {
+    if ((spp & (spp - 1u)) == 0u) {
+        const float r = __uint_as_float((127u - (31u - (uint32_t)__clz(spp))) << 23);  // 2^-log2(spp), exact
+        return F3{acc.x * r, acc.y * r, acc.z * r};
+    }
+    const float m = (float)spp;
+    return F3{acc.x / m, acc.y / m, acc.z / m};
+}
+
 // (out: the launch's output base; pixel path / spp + pix0 of it)
 __device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32_t path, bool valid,
                                                 void* __restrict__ out, size_t pix0) {
@@ -67,10 +78,7 @@ __device__ __forceinline__ void resolve_in_wave(const TileJob& job, F3 s, uint32
         for (uint32_t k = 1; k < spp; ++k)
             acc = acc + F3{__shfl(s.x, (int)(lane + k)), __shfl(s.y, (int)(lane + k)), __shfl(s.z, (int)(lane + k))};
     }
-    if (valid && (lane & (spp - 1)) == 0) {
-        const float m = (float)spp;
-        store_pixel(job, out, pix0 + path / spp, F3{acc.x / m, acc.y / m, acc.z / m});
-    }
+    if (valid && (lane & (spp - 1)) == 0) store_pixel(job, out, pix0 + path / spp, pixel_mean(acc, spp));
 }
 
 }  // namespace mm

@@ -1064,13 +1064,13 @@ __global__ void k_resolve(TileJob job, const Sample* __restrict__ samples, void*
         acc = s[0];
         for (uint32_t k = 1; k < spp; ++k) acc = acc + s[k];
     }
-    const float m = (float)spp;
-    store_pixel(job, out, pix, F3{acc.x / m, acc.y / m, acc.z / m});
+    store_pixel(job, out, pix, pixel_mean(acc, spp));
 }
 
 // The same reduction when 64 % spp == 0, a wave per 64 consecutive samples
 // (64/spp whole pixels): every load is one coalesced 1-KB wave access, and
-// resolve_in_wave adds in k_resolve's order (bit-identical).
+// resolve_in_wave adds in k_resolve's order (bit-identical).  Used for spp 1,
+// 2, 4 (spp % 8 == 0 takes k_resolve8).
 __global__ __launch_bounds__(256) void k_resolve_wave(TileJob job, const Sample* __restrict__ samples,
                                                       void* __restrict__ out) {
     const uint32_t n = job.w * job.h * job.e.spp;
@@ -1080,9 +1080,32 @@ __global__ __launch_bounds__(256) void k_resolve_wave(TileJob job, const Sample*
     resolve_in_wave(job, v, path, valid, out, 0);
 }
 
+// spp % 8 == 0: one thread per pixel, each block of 8 samples read as six
+// 16-B loads (a pixel's samples are 96 B-aligned runs: 12 spp B per pixel),
+// added in k_resolve's tree -- no cross-lane shuffles, one active lane per
+// pixel instead of one in eight (mean: pixel_mean, mm_wave_util.h).
+__global__ __launch_bounds__(256) void k_resolve8(TileJob job, const Sample* __restrict__ samples,
+                                                  void* __restrict__ out) {
+    const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= job.w * job.h) return;
+    const uint32_t spp = job.e.spp;
+    const float4* q = reinterpret_cast<const float4*>(samples + (size_t)pix * spp);
+    F3 acc;
+    for (uint32_t b = 0; b < spp; b += 8, q += 6) {
+        const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4], a5 = q[5];
+        const F3 s0{a0.x, a0.y, a0.z}, s1{a0.w, a1.x, a1.y}, s2{a1.z, a1.w, a2.x}, s3{a2.y, a2.z, a2.w};
+        const F3 s4{a3.x, a3.y, a3.z}, s5{a3.w, a4.x, a4.y}, s6{a4.z, a4.w, a5.x}, s7{a5.y, a5.z, a5.w};
+        const F3 blk = ((s0 + s1) + (s2 + s3)) + ((s4 + s5) + (s6 + s7));
+        acc = (b == 0) ? blk : acc + blk;
+    }
+    store_pixel(job, out, pix, pixel_mean(acc, spp));
+}
+
 hipError_t launch_resolve(const TileJob& job, const Sample* samples, void* out, hipStream_t s) {
     const uint32_t n = job.w * job.h;
-    if (64 % job.e.spp == 0) {
+    if (job.e.spp % 8 == 0) {
+        hipLaunchKernelGGL(k_resolve8, dim3((n + 255) / 256), dim3(256), 0, s, job, samples, out);
+    } else if (64 % job.e.spp == 0) {
         const uint32_t paths = n * job.e.spp;
         hipLaunchKernelGGL(k_resolve_wave, dim3((paths + 255) / 256), dim3(256), 0, s, job, samples, out);
     } else {
