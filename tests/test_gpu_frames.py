@@ -257,6 +257,30 @@ def test_camera_sweep(gpu, maze_n, bl, ml):
     r.close()
 
 
+@pytest.mark.parametrize("spp", [16, 24, 40])
+def test_staged_resolve_spp_multiples_of_eight(gpu, spp):
+    """k_resolve8 (one thread per pixel for spp % 8 == 0): 16 (a power of two:
+    the mean as an exact multiply), 24 and 40 (the IEEE division; 64 % spp !=
+    0, so no fused resolve either) through forced deferral, every pixel vs the
+    oracle."""
+    from mirror_maze import MM_PIPE_AUTO, Renderer, default_uniform, make_ext
+    from oracle.oracle import Oracle
+
+    s = _scene(16)
+    u = default_uniform(96, 54, 0)
+    e = make_ext(spp, 8, 8, frame=5)
+    ref, n = oracle_tile(Oracle.from_scene(s), u, e, 0, 0, 96, 54)
+    r = Renderer(0)
+    r.set_pipeline(MM_PIPE_AUTO)
+    r.set_option(21, 32)
+    r.set_option(22, 0)
+    r.upload_scene(s)
+    got, st = r.trace_tile(u, e, 0, 0, 96, 54, stats=True)
+    assert _diff(got.cpu().numpy(), ref) == 0
+    assert st.rays == n
+    r.close()
+
+
 @pytest.mark.parametrize("bl,ml", [(40, 40), (3, 200)], ids=["long-paths", "mirror-chains"])
 def test_long_paths_through_the_tail_rings(gpu, bl, ml):
     """Paths parked in the tail rings and resumed carry their state in a 64-B
